@@ -1,0 +1,205 @@
+/*
+ * ldsp.h -- C ABI of libldsp, the MI355X (gfx950) streaming-DSP library that
+ * replaces the liquid-dsp calls behind python-liquiddsp's hot path.
+ *
+ * Every entry point below names the reference interface it replaces
+ * (colbyAtCRI/python-liquiddsp, paths relative to the repository root) and the
+ * liquid-dsp routine that interface calls.  The pybind11 module `liquiddsp`
+ * (python-liquiddsp_amd/pybind/liquiddsp_module.cpp) binds these with the same
+ * class names, keyword arguments and properties as src/wrapper.cpp; a ctypes or
+ * other FFI binding can call them directly.
+ *
+ * Conventions
+ *  - All functions return LDSP_OK (0) or a negative LDSP_E* code; the message
+ *    of the last failure on the calling thread is ldsp_last_error().
+ *  - Handles are independent; calls on one handle must not overlap in time and
+ *    must be issued on one stream (or be externally ordered).
+ *  - Sample buffers: complex samples are interleaved float32 (re, im) =
+ *    numpy.complex64; real samples float32.  `mem` says whether x / y are host
+ *    pointers (LDSP_MEM_HOST: the call stages through the device and returns
+ *    after the result is in y) or device pointers (LDSP_MEM_DEVICE: the call
+ *    only enqueues work on `stream` (a hipStream_t, NULL = default stream) and
+ *    returns immediately).
+ *  - Streaming state (filter history, resampler / NCO phase, IIR state, AGC
+ *    gain, PLL) lives in device memory owned by the handle and carries across
+ *    calls exactly like the liquid objects' internal state.
+ *  - Objects can be created and configured without a GPU (design, properties,
+ *    freqresponse are host-side); device memory is allocated on first execute.
+ */
+#ifndef LDSP_H
+#define LDSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDSP_OK      0
+#define LDSP_EINVAL (-1)   /* invalid configuration / argument (Python ValueError) */
+#define LDSP_ENOMEM (-2)   /* allocation failure */
+#define LDSP_EHIP   (-3)   /* HIP runtime failure or no GPU (Python RuntimeError) */
+#define LDSP_ERANGE (-4)   /* output capacity too small */
+#define LDSP_EUNSUP (-5)   /* configuration not implemented */
+
+#define LDSP_MEM_HOST   0
+#define LDSP_MEM_DEVICE 1
+
+/* execution modes (exact = bit-identical to the sequential CPU restatement) */
+#define LDSP_MODE_FAST  0
+#define LDSP_MODE_EXACT 1
+
+const char *ldsp_last_error(void);
+int ldsp_version(void);
+int ldsp_device_count(int *n);
+int ldsp_stream_synchronize(void *stream);
+
+/* Test hook: evaluate the loop transcendentals (ldsp_math.hpp) on the device.
+ * fn: 0 exp, 1 log, 2 atan2(a, b), 3 tanh, 4 constrain (y as uint32 bits).
+ * a, b, y are device pointers of n floats. */
+int ldsp_debug_math_eval(int fn, const float *a, const float *b, float *y, size_t n, void *stream);
+
+/* ------------------------------------------------------------------------
+ * FIR filter: firfilt_rrrf (cplx=0) / firfilt_crcf (cplx=1), real taps.
+ * Replaces RealFIRFilter (src/firfilter.hpp:13-35, firfilt_rrrf_create /
+ * firfilt_rrrf_execute_block), RealDCBlocker (firfilter.hpp:42-44,
+ * firfilt_rrrf_create_dc_blocker), RealKaiserBessel (firfilter.hpp:56-61,
+ * firfilt_rrrf_create_kaiser + set_scale) and the crcf filter used inside
+ * demod.hpp:105,135-136 (new class ComplexFIRFilter).
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_firfilt_s *ldsp_firfilt_t;
+int ldsp_firfilt_create(const float *h, unsigned int n, int cplx, ldsp_firfilt_t *q);
+int ldsp_firfilt_create_kaiser(unsigned int n, float fc, float as, float mu, int cplx, ldsp_firfilt_t *q);
+int ldsp_firfilt_create_dc_blocker(unsigned int m, float as, int cplx, ldsp_firfilt_t *q);
+int ldsp_firfilt_destroy(ldsp_firfilt_t q);
+int ldsp_firfilt_reset(ldsp_firfilt_t q);
+int ldsp_firfilt_set_scale(ldsp_firfilt_t q, float scale);
+int ldsp_firfilt_get_scale(ldsp_firfilt_t q, float *scale);
+int ldsp_firfilt_get_length(ldsp_firfilt_t q, unsigned int *n);
+int ldsp_firfilt_get_taps(ldsp_firfilt_t q, float *h);
+int ldsp_firfilt_set_mode(ldsp_firfilt_t q, int mode);
+/* firfilt_*_freqresponse (firfilter.hpp:23-27) */
+int ldsp_firfilt_freqresponse(ldsp_firfilt_t q, float f, float *re, float *im);
+/* firfilt_*_execute_block (firfilter.hpp:29-35): y[i] = scale * sum_k h[k] x[i-k] */
+int ldsp_firfilt_execute(ldsp_firfilt_t q, const void *x, size_t n, void *y, int mem, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Arbitrary-rate polyphase resampler: resamp_rrrf (cplx=0) / resamp_cccf
+ * (cplx=1).  Replaces RealResampler / ComplexResampler
+ * (src/resampler.hpp:72-173: resamp_*_create(rate, m, fc, As, npfb),
+ * resamp_*_execute per sample, set_rate, reset, print).
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_resamp_s *ldsp_resamp_t;
+int ldsp_resamp_create(float rate, unsigned int m, float fc, float as, unsigned int npfb, int cplx,
+                       ldsp_resamp_t *q);
+int ldsp_resamp_destroy(ldsp_resamp_t q);
+int ldsp_resamp_reset(ldsp_resamp_t q);
+int ldsp_resamp_set_rate(ldsp_resamp_t q, float rate);
+int ldsp_resamp_get_rate(ldsp_resamp_t q, float *rate);
+/* npfb (after power-of-two rounding), step, current phase, taps per branch */
+int ldsp_resamp_get_info(ldsp_resamp_t q, unsigned int *npfb, uint32_t *step, uint32_t *phase,
+                         unsigned int *sub_len);
+int ldsp_resamp_get_taps(ldsp_resamp_t q, float *h, unsigned int cap, unsigned int *n);
+/* number of outputs the next execute of n inputs will produce (host-side, exact) */
+int ldsp_resamp_num_outputs(ldsp_resamp_t q, size_t n, size_t *nout);
+int ldsp_resamp_execute(ldsp_resamp_t q, const void *x, size_t n, void *y, size_t cap, size_t *nout,
+                        int mem, void *stream);
+
+/* ------------------------------------------------------------------------
+ * NCO: nco_crcf (type 0 = LIQUID_NCO table, 1 = LIQUID_VCO).  Replaces NCO
+ * (src/nco.hpp:4-81): frequency / phase accessors, PLL helpers and
+ * nco_crcf_mix_block_up / _down (nco.hpp:66-80).
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_nco_s *ldsp_nco_t;
+int ldsp_nco_create(int type, ldsp_nco_t *q);
+int ldsp_nco_destroy(ldsp_nco_t q);
+int ldsp_nco_reset(ldsp_nco_t q);
+int ldsp_nco_set_frequency(ldsp_nco_t q, float f);
+int ldsp_nco_get_frequency(ldsp_nco_t q, float *f);
+int ldsp_nco_adjust_frequency(ldsp_nco_t q, float df);
+int ldsp_nco_set_phase(ldsp_nco_t q, float phi);
+int ldsp_nco_get_phase(ldsp_nco_t q, float *phi);
+int ldsp_nco_adjust_phase(ldsp_nco_t q, float dphi);
+int ldsp_nco_pll_set_bandwidth(ldsp_nco_t q, float bw);
+int ldsp_nco_pll_step(ldsp_nco_t q, float dphi);
+int ldsp_nco_get_state(ldsp_nco_t q, uint32_t *theta, uint32_t *dtheta);
+int ldsp_nco_set_state(ldsp_nco_t q, uint32_t theta, uint32_t dtheta);
+int ldsp_nco_mix(ldsp_nco_t q, const void *x, size_t n, void *y, int down, int mem, void *stream);
+
+/* ------------------------------------------------------------------------
+ * IIR filter: iirfilt_rrrf (cplx=0) / iirfilt_crcf (cplx=1).  Replaces
+ * ComplexIIRFilter / RealIIRFilter (src/iirfilter.hpp:243-356,
+ * iirfilt_*_create_prototype(..., LIQUID_IIRDES_SOS, ...)), the
+ * C/R{Lowpass,Highpass,Bandpass,Bandstop}IIR family (iirfilter.hpp:61-241),
+ * CIIRFilter / RIIRFilter raw transfer functions (iirfilter.hpp:30-34,140-144,
+ * iirfilt_*_create) and DeemphasisFilter (iirfilter.hpp:358-392).
+ * ftype: 0 butter 1 cheby1 2 cheby2 3 ellip 4 bessel;
+ * btype: 0 lowpass 1 highpass 2 bandpass 3 bandstop.
+ * Mode FAST evaluates the cascade as a chunked linear scan in float64 (more
+ * accurate than liquid's float32 recursion); EXACT runs the float32 direct-form
+ * II recursion sequentially (bit-identical to the restatement).
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_iirfilt_s *ldsp_iirfilt_t;
+int ldsp_iirfilt_create_prototype(int ftype, int btype, unsigned int order, float fc, float f0,
+                                  float ap, float as, int cplx, ldsp_iirfilt_t *q);
+int ldsp_iirfilt_create_sos(const float *B, const float *A, unsigned int nsos, int cplx,
+                            ldsp_iirfilt_t *q);
+int ldsp_iirfilt_create_tf(const float *b, unsigned int nb, const float *a, unsigned int na, int cplx,
+                           ldsp_iirfilt_t *q);
+int ldsp_iirfilt_destroy(ldsp_iirfilt_t q);
+int ldsp_iirfilt_reset(ldsp_iirfilt_t q);
+int ldsp_iirfilt_set_mode(ldsp_iirfilt_t q, int mode);
+int ldsp_iirfilt_get_nsos(ldsp_iirfilt_t q, unsigned int *nsos);
+int ldsp_iirfilt_get_sos(ldsp_iirfilt_t q, float *B, float *A);
+int ldsp_iirfilt_freqresponse(ldsp_iirfilt_t q, float f, float *re, float *im);
+int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void *x, size_t n, void *y, int mem, void *stream);
+
+/* ------------------------------------------------------------------------
+ * AGC: agc_crcf.  Replaces AGC (src/agc.hpp:4-149).  execute implements
+ * AGC::execute (agc.hpp:109-128): agc_crcf_execute per sample, squelch status
+ * polled per sample, output zeroed in SIGNALLO / ENABLED.  When `status` is
+ * non-NULL it receives the per-sample squelch status (host array of n bytes;
+ * the call then synchronises) so the caller can replay onRise callbacks.
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_agc_s *ldsp_agc_t;
+int ldsp_agc_create(ldsp_agc_t *q);
+int ldsp_agc_destroy(ldsp_agc_t q);
+int ldsp_agc_reset(ldsp_agc_t q);
+int ldsp_agc_set_bandwidth(ldsp_agc_t q, float bw);
+int ldsp_agc_get_bandwidth(ldsp_agc_t q, float *bw);
+int ldsp_agc_lock(ldsp_agc_t q, int on);
+int ldsp_agc_squelch_enable(ldsp_agc_t q, int on);
+int ldsp_agc_squelch_set_threshold(ldsp_agc_t q, float t);
+int ldsp_agc_squelch_get_threshold(ldsp_agc_t q, float *t);
+int ldsp_agc_squelch_set_timeout(ldsp_agc_t q, unsigned int t);
+int ldsp_agc_squelch_get_status(ldsp_agc_t q, int *status);
+int ldsp_agc_get_gain(ldsp_agc_t q, float *g);
+int ldsp_agc_set_gain(ldsp_agc_t q, float g);
+int ldsp_agc_get_scale(ldsp_agc_t q, float *s);
+int ldsp_agc_set_scale(ldsp_agc_t q, float s);
+int ldsp_agc_get_signal_level(ldsp_agc_t q, float *x);
+int ldsp_agc_set_signal_level(ldsp_agc_t q, float x);
+int ldsp_agc_get_rssi(ldsp_agc_t q, float *r);
+int ldsp_agc_set_rssi(ldsp_agc_t q, float r);
+int ldsp_agc_set_mode(ldsp_agc_t q, int mode);
+int ldsp_agc_execute(ldsp_agc_t q, const void *x, size_t n, void *y, uint8_t *status, int mem,
+                     void *stream);
+
+/* ------------------------------------------------------------------------
+ * AM demodulator: ampmodem (type 0 dsb, 1 usb, 2 lsb).  Replaces AmpModem
+ * (src/demod.hpp:221-307: ampmodem_create(mod, type, suppressed_carrier),
+ * ampmodem_demodulate_block, ampmodem_reset).
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_ampmodem_s *ldsp_ampmodem_t;
+int ldsp_ampmodem_create(float mod_index, int type, int suppressed_carrier, ldsp_ampmodem_t *q);
+int ldsp_ampmodem_destroy(ldsp_ampmodem_t q);
+int ldsp_ampmodem_reset(ldsp_ampmodem_t q);
+int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t *theta, uint32_t *dtheta);
+int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void *x, size_t n, void *y, int mem,
+                             void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDSP_H */

@@ -1,0 +1,1317 @@
+// capi.cpp -- the C ABI of libldsp (include/ldsp.h): object lifetime, host-side
+// design and state bookkeeping, device staging, and dispatch to the gfx950
+// kernels.  No CPU fallback exists: every execute runs on a HIP device and
+// fails with LDSP_EHIP when none is present.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "design.hpp"
+#include "kernels.hpp"
+#include "ldsp_common.hpp"
+
+namespace ldsp {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+int current_device()
+{
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) throw Error(LDSP_EHIP, "no HIP device available (libldsp has no CPU fallback)");
+    int d = 0;
+    LDSP_HIP(hipGetDevice(&d));
+    return d;
+}
+
+hipStream_t library_stream(int device)
+{
+    static std::mutex mu;
+    static std::vector<hipStream_t> streams;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)streams.size() <= device) streams.resize(device + 1, nullptr);
+    if (!streams[device]) {
+        DeviceGuard g(device);
+        LDSP_HIP(hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking));
+    }
+    return streams[device];
+}
+
+// Resolve where a call runs: host-memory calls use the library stream and stage
+// through grow-only device buffers owned by the object.
+struct Exec {
+    int device;
+    hipStream_t stream;
+    bool host;
+};
+
+static Exec make_exec(int device, int mem, void* stream)
+{
+    LDSP_REQUIRE(mem == LDSP_MEM_HOST || mem == LDSP_MEM_DEVICE, "mem must be LDSP_MEM_HOST or LDSP_MEM_DEVICE");
+    Exec e;
+    e.device = device;
+    e.host = (mem == LDSP_MEM_HOST);
+    e.stream = e.host ? library_stream(device) : (hipStream_t)stream;
+    return e;
+}
+
+template <typename T>
+static T* upload(DevBuf& b, const std::vector<T>& v, int dev)
+{
+    b.ensure(std::max<size_t>(v.size(), 1) * sizeof(T), dev);
+    if (!v.empty()) LDSP_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return b.as<T>();
+}
+
+// Host <-> device staging for LDSP_MEM_HOST calls
+struct Staging {
+    DevBuf in, out;
+    const void* dev_in(const Exec& e, const void* x, size_t bytes)
+    {
+        if (!e.host) return x;
+        in.ensure(bytes, e.device);
+        if (bytes) LDSP_HIP(hipMemcpyAsync(in.p, x, bytes, hipMemcpyHostToDevice, e.stream));
+        return in.p;
+    }
+    void* dev_out(const Exec& e, void* y, size_t bytes)
+    {
+        if (!e.host) return y;
+        return out.ensure(bytes, e.device);
+    }
+    void finish(const Exec& e, void* y, size_t bytes)
+    {
+        if (!e.host) return;
+        if (bytes) LDSP_HIP(hipMemcpyAsync(y, out.p, bytes, hipMemcpyDeviceToHost, e.stream));
+        LDSP_HIP(hipStreamSynchronize(e.stream));
+    }
+};
+
+// ====================================================================== FIR
+struct FirObj {
+    std::vector<float> h;
+    bool cplx = false;
+    float scale = 1.0f;
+    int mode = LDSP_MODE_FAST;
+    int device = -1;
+    DevBuf taps_pad, taps_rev, hist[2];
+    int cur = 0;
+    hipStream_t last = nullptr;
+    Staging stg;
+    size_t esz() const { return cplx ? 8 : 4; }
+    void ensure_device()
+    {
+        if (device >= 0) return;
+        const int dev = current_device();
+        const int L = (int)h.size();
+        std::vector<float> pad((L + 15) / 16 * 16, 0.0f), rev(L);
+        for (int i = 0; i < L; i++) {
+            pad[i] = h[i];
+            rev[L - 1 - i] = h[i];
+        }
+        upload(taps_pad, pad, dev);
+        upload(taps_rev, rev, dev);
+        for (auto& b : hist) {
+            b.ensure(std::max<size_t>(L - 1, 1) * esz(), dev);
+            LDSP_HIP(hipMemset(b.p, 0, std::max<size_t>(L - 1, 1) * esz()));
+        }
+        device = dev;
+    }
+};
+} // namespace ldsp
+
+struct ldsp_firfilt_s : ldsp::FirObj {};
+struct ldsp_resamp_s;
+struct ldsp_nco_s;
+struct ldsp_iirfilt_s;
+struct ldsp_agc_s;
+struct ldsp_ampmodem_s;
+
+namespace ldsp {
+
+// ====================================================================== resampler
+struct ResampObj {
+    bool cplx = true;
+    float rate = 1.0f;
+    unsigned int m = 0, npfb = 0, sub_len = 0;
+    int bits_index = 0;
+    uint32_t step = 0;
+    uint64_t phase = 0;
+    float fc = 0, as = 0;
+    std::vector<float> hproto, sub;   // sub: [npfb][sub_len] reversed (complex interleaved if cplx)
+    int device = -1;
+    DevBuf dsub, hist[2];
+    int cur = 0;
+    hipStream_t last = nullptr;
+    Staging stg;
+    size_t esz() const { return cplx ? 8 : 4; }
+    void set_rate(float r)
+    {
+        LDSP_REQUIRE(r > 0, "resamp: resampling rate must be greater than zero");
+        LDSP_REQUIRE(r >= 0.004f && r <= 250.0f, "resamp: resampling rate must be in [0.004, 250]");
+        rate = r;
+        step = (uint32_t)round((double)((float)(1 << 24) / rate));
+    }
+    size_t num_outputs(size_t n) const
+    {
+        if (n == 0) return 0;
+        const long long num = (long long)(n - 1) * (1LL << 24) + 0xffffffLL - (long long)phase;
+        return num < 0 ? 0 : (size_t)(num / step) + 1;
+    }
+    void ensure_device()
+    {
+        if (device >= 0) return;
+        const int dev = current_device();
+        upload(dsub, sub, dev);
+        for (auto& b : hist) {
+            b.ensure(std::max<size_t>(sub_len - 1, 1) * esz(), dev);
+            LDSP_HIP(hipMemset(b.p, 0, std::max<size_t>(sub_len - 1, 1) * esz()));
+        }
+        device = dev;
+    }
+};
+
+// ====================================================================== NCO
+struct NcoObj {
+    int type = 0;
+    uint32_t theta = 0, dtheta = 0;
+    float alpha = 0.1f, beta = 0.0f;
+    std::vector<float> table;
+    int device = -1;
+    DevBuf dtab;
+    Staging stg;
+    void ensure_device()
+    {
+        if (device >= 0) return;
+        const int dev = current_device();
+        upload(dtab, table, dev);
+        device = dev;
+    }
+};
+
+static std::vector<float> nco_table()
+{
+    // nco.proto.c: sintab[i] = sinf(2.0f*M_PI*(float)(i)/1024.0f)
+    std::vector<float> t(1024);
+    for (int i = 0; i < 1024; i++) t[i] = sinf((float)(2.0f * 3.14159265358979323846 * (float)i / 1024.0f));
+    return t;
+}
+
+static uint32_t nco_constrain(float theta)
+{
+    const float p = (float)((double)theta * 0.159154943091895);
+    float f = p - (float)(long long)p;
+    if (f < 0.0f) f = (float)((double)f + 1.0);
+    return (uint32_t)(long long)(f * 4294967296.0f);
+}
+
+// ====================================================================== IIR
+struct IirObj {
+    bool cplx = true;
+    bool sos = true;
+    unsigned int nsos = 0;
+    std::vector<float> b, a;          // SOS: [nsos][3] each; TF: nb, na (normalised by a0)
+    int nb = 0, na = 0, nv = 0, D = 0;
+    int mode = LDSP_MODE_FAST;
+    int spec_W = 0;                   // > 0: fast-decaying filter -> speculative exact chunks
+    int device = -1;
+    DevBuf db, da, st32, st64, sc1, sc2, mats;
+    bool state_in64 = false;          // where the authoritative state lives
+    int plan_C = 0;
+    long plan_nch = 0;
+    int plan_G = 0;
+    hipStream_t last = nullptr;
+    Staging stg;
+    std::vector<double> A;            // D x D one-step state matrix (float64)
+
+    int fsz() const { return sos ? 3 * (int)nsos : nv; }
+    int ncomp() const { return cplx ? 2 : 1; }
+
+    // float64 step on a state vector (same layout as the scan kernels)
+    double step_host(std::vector<double>& v, double x) const
+    {
+        if (sos) {
+            double t = x;
+            for (unsigned s = 0; s < nsos; s++) {
+                const double v1 = v[2 * s], v2 = v[2 * s + 1];
+                const double v0 = t - (double)a[3 * s + 1] * v1 - (double)a[3 * s + 2] * v2;
+                t = (double)b[3 * s] * v0 + (double)b[3 * s + 1] * v1 + (double)b[3 * s + 2] * v2;
+                v[2 * s + 1] = v1;
+                v[2 * s] = v0;
+            }
+            return t;
+        }
+        double r = x;
+        for (int i = 1; i < na; i++) r -= (double)a[i] * v[i - 1];
+        double y = (double)b[0] * r;
+        for (int i = 1; i < nb; i++) y += (double)b[i] * v[i - 1];
+        for (int i = D - 1; i > 0; i--) v[i] = v[i - 1];
+        if (D > 0) v[0] = r;
+        return y;
+    }
+
+    void finalize()
+    {
+        D = sos ? 2 * (int)nsos : nv - 1;
+        A.assign((size_t)D * D, 0.0);
+        for (int c = 0; c < D; c++) {
+            std::vector<double> v(D, 0.0);
+            v[c] = 1.0;
+            step_host(v, 0.0);
+            for (int r = 0; r < D; r++) A[(size_t)r * D + c] = v[r];
+        }
+        // decay length: smallest 2^k with ||A^(2^k)||_inf < 2^-70
+        spec_W = 0;
+        if (D > 0) {
+            std::vector<double> P = A;
+            for (int k = 0; k <= 12; k++) {
+                double nrm = 0;
+                for (int r = 0; r < D; r++) {
+                    double s = 0;
+                    for (int q = 0; q < D; q++) s += fabs(P[(size_t)r * D + q]);
+                    nrm = std::max(nrm, s);
+                }
+                if (nrm < 8.5e-22) {
+                    spec_W = 2 << k;   // twice the decay length, as margin
+                    break;
+                }
+                P = matmul(P, P);
+            }
+        }
+    }
+    std::vector<double> matmul(const std::vector<double>& X, const std::vector<double>& Y) const
+    {
+        std::vector<double> Z((size_t)D * D, 0.0);
+        for (int r = 0; r < D; r++)
+            for (int k = 0; k < D; k++) {
+                const double x = X[(size_t)r * D + k];
+                for (int c = 0; c < D; c++) Z[(size_t)r * D + c] += x * Y[(size_t)k * D + c];
+            }
+        return Z;
+    }
+    std::vector<double> matpow(std::vector<double> X, uint64_t e) const
+    {
+        std::vector<double> R((size_t)D * D, 0.0);
+        for (int i = 0; i < D; i++) R[(size_t)i * D + i] = 1.0;
+        while (e) {
+            if (e & 1) R = matmul(R, X);
+            X = matmul(X, X);
+            e >>= 1;
+        }
+        return R;
+    }
+    void ensure_device()
+    {
+        if (device >= 0) return;
+        const int dev = current_device();
+        upload(db, b, dev);
+        upload(da, a, dev);
+        st32.ensure(sizeof(float) * 2 * std::max(fsz(), 1), dev);
+        LDSP_HIP(hipMemset(st32.p, 0, sizeof(float) * 2 * std::max(fsz(), 1)));
+        st64.ensure(sizeof(double) * 2 * std::max(D, 1), dev);
+        LDSP_HIP(hipMemset(st64.p, 0, sizeof(double) * 2 * std::max(D, 1)));
+        state_in64 = false;
+        device = dev;
+    }
+    k::IirDesc desc() const
+    {
+        k::IirDesc d;
+        d.sos = sos ? 1 : 0;
+        d.nsos = (int)nsos;
+        d.nb = nb;
+        d.na = na;
+        d.nv = nv;
+        d.D = D;
+        d.b = db.as<float>();
+        d.a = da.as<float>();
+        return d;
+    }
+    // move the authoritative state between the float32 and float64 layouts
+    void state_to(bool to64, hipStream_t s)
+    {
+        if (state_in64 == to64) return;
+        const int nc = ncomp(), fs = fsz();
+        std::vector<float> f(2 * std::max(fs, 1), 0.0f);
+        std::vector<double> d(2 * std::max(D, 1), 0.0);
+        LDSP_HIP(hipStreamSynchronize(s));
+        if (to64) {
+            LDSP_HIP(hipMemcpy(f.data(), st32.p, f.size() * 4, hipMemcpyDeviceToHost));
+            for (int c = 0; c < nc; c++) {
+                if (sos)
+                    for (unsigned q = 0; q < nsos; q++) {
+                        d[c * D + 2 * q] = f[c * fs + 3 * q];
+                        d[c * D + 2 * q + 1] = f[c * fs + 3 * q + 1];
+                    }
+                else
+                    for (int i = 0; i < D; i++) d[c * D + i] = f[c * fs + i];
+            }
+            LDSP_HIP(hipMemcpy(st64.p, d.data(), d.size() * 8, hipMemcpyHostToDevice));
+        } else {
+            LDSP_HIP(hipMemcpy(d.data(), st64.p, d.size() * 8, hipMemcpyDeviceToHost));
+            for (int c = 0; c < nc; c++) {
+                if (sos)
+                    for (unsigned q = 0; q < nsos; q++) {
+                        f[c * fs + 3 * q] = (float)d[c * D + 2 * q];
+                        f[c * fs + 3 * q + 1] = (float)d[c * D + 2 * q + 1];
+                        f[c * fs + 3 * q + 2] = 0.0f;
+                    }
+                else
+                    for (int i = 0; i < fs; i++) f[c * fs + i] = i < D ? (float)d[c * D + i] : 0.0f;
+            }
+            LDSP_HIP(hipMemcpy(st32.p, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+        }
+        state_in64 = to64;
+    }
+    k::IirScanPlan scan_plan(size_t n)
+    {
+        int C = 64;
+        while (C < 1024 && (size_t)C * 65536 < n) C <<= 1;
+        const long nch = (long)((n + C - 1) / C);
+        const int G = (int)((nch + 1023) / 1024);
+        if (C != plan_C || G != plan_G) {
+            const std::vector<double> AC = matpow(A, (uint64_t)C);
+            std::vector<double> M = matpow(AC, (uint64_t)G);
+            std::vector<double> all(AC);
+            for (int l = 0; l < 10; l++) {
+                all.insert(all.end(), M.begin(), M.end());
+                M = matmul(M, M);
+            }
+            upload(mats, all, device);
+            plan_C = C;
+            plan_G = G;
+        }
+        plan_nch = nch;
+        const size_t need = (size_t)nch * ncomp() * D * sizeof(double);
+        sc1.ensure(need, device);
+        sc2.ensure(need, device);
+        k::IirScanPlan p;
+        p.C = C;
+        p.nchunks = nch;
+        p.G = G;
+        p.levels = 10;
+        p.AC = mats.as<double>();
+        p.AG = mats.as<double>() + (size_t)D * D;
+        p.local = sc1.as<double>();
+        p.carry = sc2.as<double>();
+        return p;
+    }
+};
+
+// ====================================================================== AGC
+struct AgcObj {
+    k::AgcState h{};                  // host mirror
+    float bandwidth = 0.01f;
+    int device = -1;
+    DevBuf dst, scratch, status;
+    bool dev_newer = false;           // device state advanced past the mirror
+    bool upload_pending = true;
+    hipStream_t last = nullptr;
+    Staging stg;
+    void init()
+    {
+        // agc_crcf_create: bandwidth 0.01, reset (g=1, y2'=1), squelch disabled,
+        // threshold 0, timeout 100, scale 1
+        bandwidth = 0.01f;
+        h.alpha = bandwidth;
+        h.g = 1.0f;
+        h.y2p = 1.0f;
+        h.locked = 0;
+        h.mode = 7;
+        h.threshold = 0.0f;
+        h.timeout = 100;
+        h.timer = 0;
+        h.scale = 1.0f;
+    }
+    void pull()
+    {
+        if (!dev_newer) return;
+        LDSP_HIP(hipStreamSynchronize(last));
+        DeviceGuard g(device);
+        LDSP_HIP(hipMemcpy(&h, dst.p, sizeof(h), hipMemcpyDeviceToHost));
+        dev_newer = false;
+    }
+    void modified() { upload_pending = true; }
+    void ensure_device()
+    {
+        if (device >= 0) return;
+        const int dev = current_device();
+        dst.ensure(sizeof(k::AgcState), dev);
+        device = dev;
+        upload_pending = true;
+    }
+};
+
+// ====================================================================== AmpModem
+struct AmpObj {
+    float mod_index = 0.75f;
+    int type = 0;
+    int suppressed = 1;
+    unsigned int m = 25;
+    std::vector<float> lp, dc, table;
+    k::AmpState st{};
+    int device = -1;
+    DevBuf dlp, ddc, dtab, dst, lph[2], dch[2], dlh[2], x0, mb, pll;
+    int cur = 0;
+    bool dev_newer = false;
+    hipStream_t last = nullptr;
+    Staging stg;
+    void reset_host()
+    {
+        st.theta = 0;
+        st.dtheta = 0;
+        st.alpha = 0.001f;
+        st.beta = sqrtf(st.alpha);
+    }
+    void ensure_device()
+    {
+        if (device >= 0) return;
+        const int dev = current_device();
+        std::vector<float> lr(lp.rbegin(), lp.rend()), dr(dc.rbegin(), dc.rend());
+        upload(dlp, lr, dev);
+        upload(ddc, dr, dev);
+        upload(dtab, table, dev);
+        dst.ensure(sizeof(k::AmpState), dev);
+        LDSP_HIP(hipMemcpy(dst.p, &st, sizeof(st), hipMemcpyHostToDevice));
+        for (int i = 0; i < 2; i++) {
+            lph[i].ensure((2 * m) * 8, dev);
+            LDSP_HIP(hipMemset(lph[i].p, 0, (2 * m) * 8));
+            dch[i].ensure((2 * m) * 4, dev);
+            LDSP_HIP(hipMemset(dch[i].p, 0, (2 * m) * 4));
+            dlh[i].ensure(m * 8, dev);
+            LDSP_HIP(hipMemset(dlh[i].p, 0, m * 8));
+        }
+        device = dev;
+    }
+};
+
+} // namespace ldsp
+
+struct ldsp_resamp_s : ldsp::ResampObj {};
+struct ldsp_nco_s : ldsp::NcoObj {};
+struct ldsp_iirfilt_s : ldsp::IirObj {};
+struct ldsp_agc_s : ldsp::AgcObj {};
+struct ldsp_ampmodem_s : ldsp::AmpObj {};
+
+using namespace ldsp;
+
+// Run `fn` translating exceptions into status codes
+template <typename F>
+static int guard(F&& fn)
+{
+    try {
+        fn();
+        return LDSP_OK;
+    } catch (const Error& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_last_error("out of host memory");
+        return LDSP_ENOMEM;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return LDSP_EHIP;
+    }
+}
+
+#define NONNULL(p) LDSP_REQUIRE((p) != nullptr, #p " must not be NULL")
+
+extern "C" {
+
+const char* ldsp_last_error(void) { return g_last_error.c_str(); }
+int ldsp_version(void) { return 100; }
+
+int ldsp_device_count(int* n)
+{
+    return guard([&] {
+        NONNULL(n);
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+        *n = c;
+    });
+}
+
+int ldsp_stream_synchronize(void* stream)
+{
+    return guard([&] { LDSP_HIP(hipStreamSynchronize((hipStream_t)stream)); });
+}
+
+int ldsp_debug_math_eval(int fn, const float* a, const float* b, float* y, size_t n, void* stream)
+{
+    return guard([&] {
+        LDSP_REQUIRE(fn >= 0 && fn <= 4, "math_eval: unknown function");
+        (void)current_device();
+        k::math_eval(fn, a, b ? b : a, y, n, (hipStream_t)stream);
+    });
+}
+
+// ---------------------------------------------------------------- FIR
+static int fir_make(std::vector<float> h, int cplx, ldsp_firfilt_t* q)
+{
+    LDSP_REQUIRE(!h.empty(), "firfilt: filter length must be > 0");
+    LDSP_REQUIRE((int)h.size() <= k::kFirMaxTaps, "firfilt: filter length exceeds 8192 taps");
+    auto* o = new ldsp_firfilt_s();
+    o->h = std::move(h);
+    o->cplx = cplx != 0;
+    *q = o;
+    return LDSP_OK;
+}
+
+int ldsp_firfilt_create(const float* h, unsigned int n, int cplx, ldsp_firfilt_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(h != nullptr || n == 0, "firfilt: taps must not be NULL");
+        fir_make(std::vector<float>(h, h + n), cplx, q);
+    });
+}
+
+int ldsp_firfilt_create_kaiser(unsigned int n, float fc, float as, float mu, int cplx, ldsp_firfilt_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        fir_make(design::firdes_kaiser(n, fc, as, mu), cplx, q);
+    });
+}
+
+int ldsp_firfilt_create_dc_blocker(unsigned int m, float as, int cplx, ldsp_firfilt_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        fir_make(design::firdes_notch(m, 0.0f, as), cplx, q);
+    });
+}
+
+int ldsp_firfilt_destroy(ldsp_firfilt_t q)
+{
+    return guard([&] {
+        if (q && q->last) (void)hipStreamSynchronize(q->last);
+        delete q;
+    });
+}
+
+int ldsp_firfilt_reset(ldsp_firfilt_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (q->device < 0) return;
+        DeviceGuard g(q->device);
+        const size_t bytes = std::max<size_t>(q->h.size() - 1, 1) * q->esz();
+        for (auto& b : q->hist) LDSP_HIP(hipMemsetAsync(b.p, 0, bytes, q->last));
+    });
+}
+
+int ldsp_firfilt_set_scale(ldsp_firfilt_t q, float s) { return guard([&] { NONNULL(q); q->scale = s; }); }
+int ldsp_firfilt_get_scale(ldsp_firfilt_t q, float* s) { return guard([&] { NONNULL(q); NONNULL(s); *s = q->scale; }); }
+int ldsp_firfilt_get_length(ldsp_firfilt_t q, unsigned int* n)
+{
+    return guard([&] { NONNULL(q); NONNULL(n); *n = (unsigned)q->h.size(); });
+}
+int ldsp_firfilt_get_taps(ldsp_firfilt_t q, float* h)
+{
+    return guard([&] { NONNULL(q); NONNULL(h); std::copy(q->h.begin(), q->h.end(), h); });
+}
+int ldsp_firfilt_set_mode(ldsp_firfilt_t q, int mode)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(mode == LDSP_MODE_FAST || mode == LDSP_MODE_EXACT, "unknown mode");
+        q->mode = mode;
+    });
+}
+
+// liquid firfilt_freqresponse: H = scale * sum_i hrev[i] exp(+j 2 pi f i)
+int ldsp_firfilt_freqresponse(ldsp_firfilt_t q, float f, float* re, float* im)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(re);
+        NONNULL(im);
+        const size_t L = q->h.size();
+        std::complex<float> H(0.0f, 0.0f);
+        for (size_t i = 0; i < L; i++) {
+            const float hr = q->h[L - 1 - i];
+            const float ang = (float)(2 * 3.14159265358979323846 * (double)f * (double)i);
+            H += hr * std::exp(std::complex<float>(0.0f, ang));
+        }
+        H *= q->scale;
+        *re = H.real();
+        *im = H.imag();
+    });
+}
+
+int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "firfilt_execute: NULL buffer");
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const size_t bytes = n * q->esz();
+        const void* dx = q->stg.dev_in(e, x, bytes);
+        void* dy = q->stg.dev_out(e, y, bytes);
+        const int L = (int)q->h.size();
+        void* hin = q->hist[q->cur].p;
+        void* hout = q->hist[1 - q->cur].p;
+        if (L > 1 || n > 0) {
+            if (q->mode == LDSP_MODE_EXACT)
+                k::fir_exact(q->cplx, dx, hin, hout, n, q->taps_rev.as<float>(), L, q->scale, dy, e.stream);
+            else
+                k::fir_fast(q->cplx, dx, hin, hout, n, q->taps_pad.as<float>(), L, q->scale, dy, e.stream);
+            if (L > 1) q->cur = 1 - q->cur;
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, bytes);
+    });
+}
+
+// ---------------------------------------------------------------- resampler
+int ldsp_resamp_create(float rate, unsigned int m, float fc, float as, unsigned int npfb, int cplx, ldsp_resamp_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(m > 0, "resamp: filter semi-length must be greater than zero");
+        LDSP_REQUIRE(fc > 0.0f && fc < 0.5f, "resamp: filter cutoff must be in (0, 0.5)");
+        LDSP_REQUIRE(as > 0.0f, "resamp: filter stop-band suppression must be greater than zero");
+        LDSP_REQUIRE(npfb > 0, "resamp: number of filters must be greater than zero");
+        std::unique_ptr<ldsp_resamp_s> o(new ldsp_resamp_s());
+        o->cplx = cplx != 0;
+        o->set_rate(rate);
+        o->m = m;
+        o->fc = fc;
+        o->as = as;
+        unsigned int bits = 0;
+        for (unsigned int v = npfb - 1; v; v >>= 1) bits++;   // liquid_nextpow2
+        LDSP_REQUIRE(bits <= 16, "resamp: too many filters");
+        o->npfb = 1u << bits;
+        o->bits_index = 24 - (int)bits;
+        const unsigned int n = 2 * m * o->npfb + 1;
+        std::vector<float> hf = design::firdes_kaiser(n, fc / ((float)o->npfb), as, 0.0f);
+        float gain = 0.0f;
+        for (float v : hf) gain += v;
+        gain = (float)o->npfb / gain;
+        o->hproto.resize(n);
+        for (unsigned int i = 0; i < n; i++) o->hproto[i] = hf[i] * gain;
+        o->sub_len = (n - 1) / o->npfb;
+        const unsigned c = o->cplx ? 2 : 1;
+        o->sub.assign((size_t)o->npfb * o->sub_len * c, 0.0f);
+        for (unsigned int b = 0; b < o->npfb; b++)
+            for (unsigned int k = 0; k < o->sub_len; k++)
+                o->sub[((size_t)b * o->sub_len + (o->sub_len - k - 1)) * c] = o->hproto[b + k * o->npfb];
+        *q = o.release();
+    });
+}
+
+int ldsp_resamp_destroy(ldsp_resamp_t q)
+{
+    return guard([&] {
+        if (q && q->last) (void)hipStreamSynchronize(q->last);
+        delete q;
+    });
+}
+
+int ldsp_resamp_reset(ldsp_resamp_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->phase = 0;
+        if (q->device < 0) return;
+        DeviceGuard g(q->device);
+        const size_t bytes = std::max<size_t>(q->sub_len - 1, 1) * q->esz();
+        for (auto& b : q->hist) LDSP_HIP(hipMemsetAsync(b.p, 0, bytes, q->last));
+    });
+}
+
+int ldsp_resamp_set_rate(ldsp_resamp_t q, float rate) { return guard([&] { NONNULL(q); q->set_rate(rate); }); }
+int ldsp_resamp_get_rate(ldsp_resamp_t q, float* r) { return guard([&] { NONNULL(q); NONNULL(r); *r = q->rate; }); }
+int ldsp_resamp_get_info(ldsp_resamp_t q, unsigned int* npfb, uint32_t* step, uint32_t* phase, unsigned int* sub_len)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (npfb) *npfb = q->npfb;
+        if (step) *step = q->step;
+        if (phase) *phase = (uint32_t)q->phase;
+        if (sub_len) *sub_len = q->sub_len;
+    });
+}
+int ldsp_resamp_get_taps(ldsp_resamp_t q, float* h, unsigned int cap, unsigned int* n)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (n) *n = (unsigned)q->hproto.size();
+        if (h) {
+            LDSP_REQUIRE(cap >= q->hproto.size(), "resamp_get_taps: capacity too small");
+            std::copy(q->hproto.begin(), q->hproto.end(), h);
+        }
+    });
+}
+int ldsp_resamp_num_outputs(ldsp_resamp_t q, size_t n, size_t* nout)
+{
+    return guard([&] { NONNULL(q); NONNULL(nout); *nout = q->num_outputs(n); });
+}
+
+int ldsp_resamp_execute(ldsp_resamp_t q, const void* x, size_t n, void* y, size_t cap, size_t* nout, int mem,
+                        void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        const size_t K = q->num_outputs(n);
+        if (nout) *nout = K;
+        if (K > cap) throw Error(LDSP_ERANGE, "resamp_execute: output capacity too small");
+        LDSP_REQUIRE(n == 0 || x, "resamp_execute: NULL input");
+        LDSP_REQUIRE(K == 0 || y, "resamp_execute: NULL output");
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const void* dx = q->stg.dev_in(e, x, n * q->esz());
+        void* dy = q->stg.dev_out(e, y, K * q->esz());
+        if (n > 0) {
+            k::ResampPlan p;
+            p.P0 = q->phase;
+            p.step = q->step;
+            p.bits_index = q->bits_index;
+            p.sub_len = (int)q->sub_len;
+            p.npfb = (int)q->npfb;
+            p.K = K;
+            int KB = 64;
+            auto span_for = [&](int kb) {
+                return (int)(((uint64_t)(kb - 1) * q->step >> 24) + 3 + q->sub_len);
+            };
+            while (KB > 1 && (size_t)span_for(KB) * q->esz() > 48 * 1024) KB >>= 1;
+            p.KB = KB;
+            p.span_max = span_for(KB);
+            k::resamp(q->cplx, dx, q->hist[q->cur].p, q->hist[1 - q->cur].p, n, q->dsub.as<float>(), p, dy,
+                      e.stream);
+            if (q->sub_len > 1) q->cur = 1 - q->cur;
+            q->phase = (uint64_t)((long long)q->phase + (long long)K * q->step - (long long)n * (1LL << 24));
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, K * q->esz());
+    });
+}
+
+// ---------------------------------------------------------------- NCO
+int ldsp_nco_create(int type, ldsp_nco_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(type == 0 || type == 1, "nco: type must be 0 (nco) or 1 (vco)");
+        auto* o = new ldsp_nco_s();
+        o->type = type;
+        o->table = nco_table();
+        o->alpha = 0.1f;                     // nco_crcf_pll_set_bandwidth(q, 0.1f) at create
+        o->beta = sqrtf(o->alpha);
+        *q = o;
+    });
+}
+int ldsp_nco_destroy(ldsp_nco_t q) { return guard([&] { delete q; }); }
+int ldsp_nco_reset(ldsp_nco_t q) { return guard([&] { NONNULL(q); q->theta = 0; q->dtheta = 0; }); }
+int ldsp_nco_set_frequency(ldsp_nco_t q, float f) { return guard([&] { NONNULL(q); q->dtheta = nco_constrain(f); }); }
+int ldsp_nco_adjust_frequency(ldsp_nco_t q, float df)
+{
+    return guard([&] { NONNULL(q); q->dtheta += nco_constrain(df); });
+}
+int ldsp_nco_set_phase(ldsp_nco_t q, float p) { return guard([&] { NONNULL(q); q->theta = nco_constrain(p); }); }
+int ldsp_nco_adjust_phase(ldsp_nco_t q, float dp) { return guard([&] { NONNULL(q); q->theta += nco_constrain(dp); }); }
+int ldsp_nco_get_frequency(ldsp_nco_t q, float* f)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(f);
+        const double kPi = 3.14159265358979323846;
+        const float d = (float)(2.0f * kPi * (double)(float)q->dtheta / (double)(float)(1ULL << 32));
+        *f = d > kPi ? (float)(d - 2 * kPi) : d;
+    });
+}
+int ldsp_nco_get_phase(ldsp_nco_t q, float* p)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(p);
+        const double kPi = 3.14159265358979323846;
+        const float t = (float)(2.0f * kPi * (double)(float)q->theta / (double)(float)(1ULL << 32));
+        *p = t > kPi ? (float)(t - 2 * kPi) : t;
+    });
+}
+int ldsp_nco_pll_set_bandwidth(ldsp_nco_t q, float bw)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(bw >= 0.0f, "nco_pll_set_bandwidth: bandwidth must be positive");
+        q->alpha = bw;
+        q->beta = sqrtf(q->alpha);
+    });
+}
+int ldsp_nco_pll_step(ldsp_nco_t q, float dphi)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->dtheta += nco_constrain(dphi * q->alpha);
+        q->theta += nco_constrain(dphi * q->beta);
+    });
+}
+int ldsp_nco_get_state(ldsp_nco_t q, uint32_t* t, uint32_t* d)
+{
+    return guard([&] { NONNULL(q); if (t) *t = q->theta; if (d) *d = q->dtheta; });
+}
+int ldsp_nco_set_state(ldsp_nco_t q, uint32_t t, uint32_t d)
+{
+    return guard([&] { NONNULL(q); q->theta = t; q->dtheta = d; });
+}
+
+int ldsp_nco_mix(ldsp_nco_t q, const void* x, size_t n, void* y, int down, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "nco_mix: NULL buffer");
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const void* dx = q->stg.dev_in(e, x, n * 8);
+        void* dy = q->stg.dev_out(e, y, n * 8);
+        k::nco_mix(dx, dy, n, q->theta, q->dtheta, q->dtab.as<float>(), down != 0, q->type, e.stream);
+        q->theta += (uint32_t)((uint64_t)n * q->dtheta);
+        q->stg.finish(e, y, n * 8);
+    });
+}
+
+// ---------------------------------------------------------------- IIR
+static void iir_finalize_sos(ldsp_iirfilt_s* o, const float* B, const float* A, unsigned nsos)
+{
+    LDSP_REQUIRE(nsos > 0 && nsos <= 8, "iirfilt: 1..8 second-order sections supported");
+    o->sos = true;
+    o->nsos = nsos;
+    o->b.resize(3 * nsos);
+    o->a.resize(3 * nsos);
+    for (unsigned s = 0; s < nsos; s++) {
+        const float a0 = A[3 * s];          // iirfiltsos_set_coefficients
+        LDSP_REQUIRE(a0 != 0.0f, "iirfilt: a0 must be non-zero");
+        for (int k = 0; k < 3; k++) {
+            o->b[3 * s + k] = B[3 * s + k] / a0;
+            o->a[3 * s + k] = A[3 * s + k] / a0;
+        }
+    }
+    o->finalize();
+}
+
+int ldsp_iirfilt_create_sos(const float* B, const float* A, unsigned int nsos, int cplx, ldsp_iirfilt_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(B);
+        NONNULL(A);
+        std::unique_ptr<ldsp_iirfilt_s> o(new ldsp_iirfilt_s());
+        o->cplx = cplx != 0;
+        iir_finalize_sos(o.get(), B, A, nsos);
+        *q = o.release();
+    });
+}
+
+int ldsp_iirfilt_create_tf(const float* b, unsigned int nb, const float* a, unsigned int na, int cplx,
+                           ldsp_iirfilt_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(b && a && nb > 0 && na > 0, "iirfilt: coefficient arrays must be non-empty");
+        LDSP_REQUIRE(nb <= 17 && na <= 17, "iirfilt: transfer functions up to order 16 supported");
+        LDSP_REQUIRE(a[0] != 0.0f, "iirfilt: a[0] must be non-zero");
+        std::unique_ptr<ldsp_iirfilt_s> o(new ldsp_iirfilt_s());
+        o->cplx = cplx != 0;
+        o->sos = false;
+        o->nb = (int)nb;
+        o->na = (int)na;
+        o->nv = (int)std::max(nb, na);
+        const float a0 = a[0];              // iirfilt_create: normalise by a[0]
+        o->b.resize(nb);
+        o->a.resize(na);
+        for (unsigned i = 0; i < nb; i++) o->b[i] = b[i] / a0;
+        for (unsigned i = 0; i < na; i++) o->a[i] = a[i] / a0;
+        o->finalize();
+        *q = o.release();
+    });
+}
+
+int ldsp_iirfilt_create_prototype(int ftype, int btype, unsigned int order, float fc, float f0, float ap, float as,
+                                  int cplx, ldsp_iirfilt_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(ftype >= 0 && ftype <= 4, "iirfilt: unknown filter type");
+        LDSP_REQUIRE(btype >= 0 && btype <= 3, "iirfilt: unknown band type");
+        design::SOS s = design::iirdes_sos(ftype, btype, order, fc, f0, ap, as);
+        std::unique_ptr<ldsp_iirfilt_s> o(new ldsp_iirfilt_s());
+        o->cplx = cplx != 0;
+        iir_finalize_sos(o.get(), s.B.data(), s.A.data(), s.nsos);
+        *q = o.release();
+    });
+}
+
+int ldsp_iirfilt_destroy(ldsp_iirfilt_t q)
+{
+    return guard([&] {
+        if (q && q->last) (void)hipStreamSynchronize(q->last);
+        delete q;
+    });
+}
+
+int ldsp_iirfilt_reset(ldsp_iirfilt_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (q->device < 0) return;
+        DeviceGuard g(q->device);
+        LDSP_HIP(hipMemsetAsync(q->st32.p, 0, q->st32.cap, q->last));
+        LDSP_HIP(hipMemsetAsync(q->st64.p, 0, q->st64.cap, q->last));
+    });
+}
+
+int ldsp_iirfilt_set_mode(ldsp_iirfilt_t q, int mode)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(mode == LDSP_MODE_FAST || mode == LDSP_MODE_EXACT, "unknown mode");
+        q->mode = mode;
+    });
+}
+int ldsp_iirfilt_get_nsos(ldsp_iirfilt_t q, unsigned int* n)
+{
+    return guard([&] { NONNULL(q); NONNULL(n); *n = q->sos ? q->nsos : 0; });
+}
+int ldsp_iirfilt_get_sos(ldsp_iirfilt_t q, float* B, float* A)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(q->sos, "iirfilt_get_sos: filter is in transfer-function form");
+        if (B) std::copy(q->b.begin(), q->b.end(), B);
+        if (A) std::copy(q->a.begin(), q->a.end(), A);
+    });
+}
+
+// liquid iirfilt_freqresponse (evaluates with exp(+j 2 pi f k))
+int ldsp_iirfilt_freqresponse(ldsp_iirfilt_t q, float f, float* re, float* im)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(re);
+        NONNULL(im);
+        using cf = std::complex<float>;
+        const double kPi = 3.14159265358979323846;
+        auto ex = [&](int k) { return std::exp(cf(0.0f, (float)(2 * kPi * (double)f * (double)k))); };
+        cf H;
+        if (!q->sos) {
+            cf Ha(0.0f, 0.0f), Hb(0.0f, 0.0f);
+            for (int i = 0; i < q->nb; i++) Hb += q->b[i] * ex(i);
+            for (int i = 0; i < q->na; i++) Ha += q->a[i] * ex(i);
+            H = Hb / Ha;
+        } else {
+            H = cf(1.0f, 0.0f);
+            for (unsigned s = 0; s < q->nsos; s++) {
+                const cf Hb = q->b[3 * s] * ex(0) + q->b[3 * s + 1] * ex(1) + q->b[3 * s + 2] * ex(2);
+                const cf Ha = q->a[3 * s] * ex(0) + q->a[3 * s + 1] * ex(1) + q->a[3 * s + 2] * ex(2);
+                H *= Hb / Ha;
+            }
+        }
+        *re = H.real();
+        *im = H.imag();
+    });
+}
+
+int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "iirfilt_execute: NULL buffer");
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const size_t bytes = n * (q->cplx ? 8 : 4);
+        const void* dx = q->stg.dev_in(e, x, bytes);
+        void* dy = q->stg.dev_out(e, y, bytes);
+        if (n > 0) {
+            const k::IirDesc d = q->desc();
+            if (q->spec_W > 0 && q->spec_W <= 4096) {
+                // fast-decaying filter: speculative exact chunks (same bits as sequential)
+                q->state_to(false, e.stream);
+                k::SpecPlan p;
+                p.W = q->spec_W;
+                p.C = std::max(256, q->spec_W);
+                p.nchunks = (long)((n + p.C - 1) / p.C);
+                const size_t need = (size_t)p.nchunks * 2 * q->ncomp() * q->fsz() * sizeof(float);
+                p.scratch = q->sc1.ensure(need, q->device);
+                k::iir_spec(q->cplx, d, dx, n, q->st32.as<float>(), p, dy, e.stream);
+            } else if (q->mode == LDSP_MODE_EXACT) {
+                q->state_to(false, e.stream);
+                k::iir_seq(q->cplx, d, dx, n, q->st32.as<float>(), dy, e.stream);
+            } else {
+                q->state_to(true, e.stream);
+                const k::IirScanPlan p = q->scan_plan(n);
+                k::iir_scan(q->cplx, d, dx, n, q->st64.as<double>(), p, dy, e.stream);
+            }
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, bytes);
+    });
+}
+
+// ---------------------------------------------------------------- AGC
+int ldsp_agc_create(ldsp_agc_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        auto* o = new ldsp_agc_s();
+        o->init();
+        *q = o;
+    });
+}
+int ldsp_agc_destroy(ldsp_agc_t q)
+{
+    return guard([&] {
+        if (q && q->last) (void)hipStreamSynchronize(q->last);
+        delete q;
+    });
+}
+
+// agc_crcf_reset: g = 1, y2' = 1, unlock, squelch ENABLED unless disabled
+int ldsp_agc_reset(ldsp_agc_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->pull();
+        q->h.g = 1.0f;
+        q->h.y2p = 1.0f;
+        q->h.locked = 0;
+        q->h.mode = (q->h.mode == 7) ? 7 : 1;
+        q->modified();
+    });
+}
+int ldsp_agc_set_bandwidth(ldsp_agc_t q, float bw)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(bw >= 0.0f && bw <= 1.0f, "agc_set_bandwidth: bandwidth must be in [0, 1]");
+        q->pull();
+        q->bandwidth = bw;
+        q->h.alpha = bw;
+        q->modified();
+    });
+}
+int ldsp_agc_get_bandwidth(ldsp_agc_t q, float* bw) { return guard([&] { NONNULL(q); NONNULL(bw); *bw = q->bandwidth; }); }
+int ldsp_agc_lock(ldsp_agc_t q, int on)
+{
+    return guard([&] { NONNULL(q); q->pull(); q->h.locked = on ? 1 : 0; q->modified(); });
+}
+int ldsp_agc_squelch_enable(ldsp_agc_t q, int on)
+{
+    return guard([&] { NONNULL(q); q->pull(); q->h.mode = on ? 1 : 7; q->modified(); });
+}
+int ldsp_agc_squelch_set_threshold(ldsp_agc_t q, float t)
+{
+    return guard([&] { NONNULL(q); q->pull(); q->h.threshold = t; q->modified(); });
+}
+int ldsp_agc_squelch_get_threshold(ldsp_agc_t q, float* t)
+{
+    return guard([&] { NONNULL(q); NONNULL(t); *t = q->h.threshold; });
+}
+int ldsp_agc_squelch_set_timeout(ldsp_agc_t q, unsigned int t)
+{
+    return guard([&] { NONNULL(q); q->pull(); q->h.timeout = t; q->modified(); });
+}
+int ldsp_agc_squelch_get_status(ldsp_agc_t q, int* s)
+{
+    return guard([&] { NONNULL(q); NONNULL(s); q->pull(); *s = q->h.mode; });
+}
+int ldsp_agc_get_gain(ldsp_agc_t q, float* g) { return guard([&] { NONNULL(q); NONNULL(g); q->pull(); *g = q->h.g; }); }
+int ldsp_agc_set_gain(ldsp_agc_t q, float g)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(g > 0.0f, "agc_set_gain: gain must be greater than zero");
+        q->pull();
+        q->h.g = g;
+        q->modified();
+    });
+}
+int ldsp_agc_get_scale(ldsp_agc_t q, float* s) { return guard([&] { NONNULL(q); NONNULL(s); *s = q->h.scale; }); }
+int ldsp_agc_set_scale(ldsp_agc_t q, float s)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(s > 0.0f, "agc_set_scale: scale must be greater than zero");
+        q->pull();
+        q->h.scale = s;
+        q->modified();
+    });
+}
+int ldsp_agc_get_signal_level(ldsp_agc_t q, float* x)
+{
+    return guard([&] { NONNULL(q); NONNULL(x); q->pull(); *x = (float)(1.0 / (double)q->h.g); });
+}
+int ldsp_agc_set_signal_level(ldsp_agc_t q, float x)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(x > 0.0f, "agc_set_signal_level: level must be greater than zero");
+        q->pull();
+        q->h.g = (float)(1.0 / (double)x);
+        q->h.y2p = 1.0f;
+        q->modified();
+    });
+}
+int ldsp_agc_get_rssi(ldsp_agc_t q, float* r)
+{
+    return guard([&] { NONNULL(q); NONNULL(r); q->pull(); *r = (float)(-20 * log10((double)q->h.g)); });
+}
+int ldsp_agc_set_rssi(ldsp_agc_t q, float r)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->pull();
+        q->h.g = powf(10.0f, -r / 20.0f);
+        if (q->h.g < 1e-16f) q->h.g = 1e-16f;
+        q->h.y2p = 1.0f;
+        q->modified();
+    });
+}
+int ldsp_agc_set_mode(ldsp_agc_t q, int mode)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(mode == LDSP_MODE_FAST || mode == LDSP_MODE_EXACT, "unknown mode");
+    });
+}
+
+int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* status, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "agc_execute: NULL buffer");
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        if (q->upload_pending) {
+            LDSP_HIP(hipStreamSynchronize(e.stream));
+            LDSP_HIP(hipMemcpy(q->dst.p, &q->h, sizeof(q->h), hipMemcpyHostToDevice));
+            q->upload_pending = false;
+        }
+        const void* dx = q->stg.dev_in(e, x, n * 8);
+        void* dy = q->stg.dev_out(e, y, n * 8);
+        uint8_t* dstat = status ? (uint8_t*)q->status.ensure(std::max<size_t>(n, 1), q->device) : nullptr;
+        if (n > 0) {
+            const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
+            const int W = (int)std::min(1 << 20, std::max(2048, (int)(64.0f / a)));
+            if (n >= (size_t)4 * W) {
+                k::SpecPlan p;
+                p.W = W;
+                p.C = 512;
+                p.nchunks = (long)((n + p.C - 1) / p.C);
+                p.scratch = q->scratch.ensure((size_t)p.nchunks * 8 * sizeof(unsigned), q->device);
+                k::agc_spec(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
+            } else {
+                k::agc_seq(dx, n, q->dst.as<k::AgcState>(), dy, dstat, e.stream);
+            }
+            q->dev_newer = true;
+        }
+        q->last = e.stream;
+        if (status && n > 0) {
+            LDSP_HIP(hipMemcpyAsync(status, dstat, n, hipMemcpyDeviceToHost, e.stream));
+            LDSP_HIP(hipStreamSynchronize(e.stream));
+        }
+        q->stg.finish(e, y, n * 8);
+    });
+}
+
+// ---------------------------------------------------------------- AmpModem
+int ldsp_ampmodem_create(float mod_index, int type, int suppressed_carrier, ldsp_ampmodem_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(type >= 0 && type <= 2, "ampmodem: type must be 0 (dsb), 1 (usb) or 2 (lsb)");
+        if (type != 0) throw Error(LDSP_EUNSUP, "ampmodem: single-sideband demodulation is not implemented");
+        std::unique_ptr<ldsp_ampmodem_s> o(new ldsp_ampmodem_s());
+        o->mod_index = mod_index;
+        o->type = type;
+        o->suppressed = suppressed_carrier != 0;
+        o->m = 25;
+        o->lp = design::firdes_kaiser(2 * o->m + 1, 0.01f, 40.0f, 0.0f);   // carrier lowpass
+        o->dc = design::firdes_notch(o->m, 0.0f, 20.0f);                     // DC blocker
+        o->table = nco_table();
+        o->reset_host();
+        *q = o.release();
+    });
+}
+int ldsp_ampmodem_destroy(ldsp_ampmodem_t q)
+{
+    return guard([&] {
+        if (q && q->last) (void)hipStreamSynchronize(q->last);
+        delete q;
+    });
+}
+int ldsp_ampmodem_reset(ldsp_ampmodem_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->reset_host();
+        q->dev_newer = false;
+        if (q->device < 0) return;
+        DeviceGuard g(q->device);
+        if (q->last) LDSP_HIP(hipStreamSynchronize(q->last));
+        LDSP_HIP(hipMemcpy(q->dst.p, &q->st, sizeof(q->st), hipMemcpyHostToDevice));
+        for (int i = 0; i < 2; i++) {
+            LDSP_HIP(hipMemset(q->lph[i].p, 0, q->lph[i].cap));
+            LDSP_HIP(hipMemset(q->dch[i].p, 0, q->dch[i].cap));
+            LDSP_HIP(hipMemset(q->dlh[i].p, 0, q->dlh[i].cap));
+        }
+    });
+}
+int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (q->dev_newer) {
+            DeviceGuard g(q->device);
+            LDSP_HIP(hipStreamSynchronize(q->last));
+            LDSP_HIP(hipMemcpy(&q->st, q->dst.p, sizeof(q->st), hipMemcpyDeviceToHost));
+            q->dev_newer = false;
+        }
+        if (t) *t = q->st.theta;
+        if (d) *d = q->st.dtheta;
+    });
+}
+
+int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "ampmodem_demodulate: NULL buffer");
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const void* dx = q->stg.dev_in(e, x, n * 8);
+        float* dy = (float*)q->stg.dev_out(e, y, n * 4);
+        if (n > 0) {
+            const int L = 2 * (int)q->m + 1;
+            void* x0 = q->x0.ensure(n * 8, q->device);
+            k::fir_exact(true, dx, q->lph[q->cur].p, q->lph[1 - q->cur].p, n, q->dlp.as<float>(), L, 1.0f, x0,
+                         e.stream);
+            float* mbuf = q->suppressed ? dy : (float*)q->mb.ensure(n * 4, q->device);
+            void* pscr = q->pll.ensure(k::pll_scratch_bytes(n), q->device);
+            k::ampmodem_pll(x0, dx, q->dlh[q->cur].p, q->dlh[1 - q->cur].p, (int)q->m, n, q->dst.as<k::AmpState>(),
+                            q->dtab.as<float>(), q->mod_index, q->suppressed ? 1 : 0, mbuf, pscr, e.stream);
+            if (!q->suppressed)
+                k::fir_exact(false, mbuf, q->dch[q->cur].p, q->dch[1 - q->cur].p, n, q->ddc.as<float>(), L, 1.0f,
+                             dy, e.stream);
+            q->cur = 1 - q->cur;
+            q->dev_newer = true;
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, n * 4);
+    });
+}
+
+} // extern "C"

@@ -1,0 +1,409 @@
+// k_fir.hip -- FIR, polyphase resampler and NCO kernels for gfx950.
+//
+// FIR (replaces firfilt_{rrrf,crcf}_execute_block behind reference
+// src/firfilter.hpp:33 and the crcf filter of demod.hpp:135):
+//   fast : 256 threads x 16 consecutive outputs per thread (4096 per block).
+//          The input tile + (L-1) halo is staged once in LDS with one pad slot
+//          every 16 samples, so each lane's sliding-window reads (lane stride
+//          17 slots) are bank-conflict free.  Taps are wave-uniform and arrive
+//          through scalar loads (SGPR operands of v_fma_f32); the window is
+//          register-blocked 16 x 16 so every LDS read feeds 16 FMAs.
+//   exact: one output per thread, liquid dotprod order (oldest sample first,
+//          separate multiply and add) -> bit-identical to the restatement.
+// Resampler (resamp_{rrrf,cccf}_execute, reference src/resampler.hpp:164-167):
+//   the host computes the output count and phase schedule in closed form
+//   (integer arithmetic), so each output's input index and polyphase branch
+//   are computed independently on the GPU; a 64-thread block stages the input
+//   span of its 64 outputs in LDS with coalesced loads.
+// NCO mix (nco_crcf_mix_block_{up,down}, reference src/nco.hpp:70,78):
+//   theta_i = theta_0 + i * dtheta (mod 2^32, exact), 1024-entry table in LDS.
+#include "kernels.hpp"
+#include "ldsp_common.hpp"
+
+namespace ldsp {
+namespace k {
+
+namespace {
+
+constexpr int kR = 16;             // outputs per thread (fast FIR)
+constexpr int kThreads = 256;
+constexpr int kTile = kR * kThreads;
+
+__host__ __device__ __forceinline__ int fslot(int e) { return e + (e >> 4); }
+
+__device__ __forceinline__ float vzero(float) { return 0.0f; }
+__device__ __forceinline__ float2 vzero(float2) { return make_float2(0.0f, 0.0f); }
+__device__ __forceinline__ float vfma(float h, float v, float a) { return fmaf(h, v, a); }
+__device__ __forceinline__ float2 vfma(float h, float2 v, float2 a)
+{
+    return make_float2(fmaf(h, v.x, a.x), fmaf(h, v.y, a.y));
+}
+__device__ __forceinline__ float vscale(float a, float s) { return a * s; }
+__device__ __forceinline__ float2 vscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// exact accumulate: r = r + h*x (no contraction: library built with -ffp-contract=off)
+__device__ __forceinline__ float vmac(float r, float h, float v) { return r + h * v; }
+__device__ __forceinline__ float2 vmac(float2 r, float h, float2 v)
+{
+    return make_float2(r.x + h * v.x, r.y + h * v.y);
+}
+
+template <typename T, bool PARTIAL>
+__device__ __forceinline__ void fir_kblock(T (&acc)[kR], T (&anew)[kR], const T (&bold)[kR], const T* lds,
+                                           int b0, const float* __restrict__ hk, int rem)
+{
+#pragma unroll
+    for (int i = 0; i < kR; i++)
+        if (!PARTIAL || i >= kR - rem) anew[i] = lds[fslot(b0 + i - (kR - 1))];
+#pragma unroll
+    for (int s = 0; s < kR; s++) {
+        const float hs = hk[s];      // taps are zero padded to a multiple of kR
+        if (!PARTIAL || s < rem) {   // wave-uniform
+#pragma unroll
+            for (int r = 0; r < kR; r++) {
+                const T v = (r > s) ? bold[r - s - 1] : anew[r - s + kR - 1];
+                acc[r] = vfma(hs, v, acc[r]);
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_fir_fast(const T* __restrict__ x, const T* __restrict__ hist,
+                                                       T* __restrict__ hist_out, long n,
+                                                       const float* __restrict__ h, int L, float scale,
+                                                       T* __restrict__ y)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* lds = reinterpret_cast<T*>(smem);
+    const long tile0 = (long)blockIdx.x * kTile;
+    const int halo = L - 1;
+    const int span = kTile + halo;
+    const int tid = threadIdx.x;
+    const T z = vzero(T());
+    for (int e = tid; e < span; e += kThreads) {
+        const long gi = tile0 - halo + e;
+        T v = z;
+        if (gi >= 0) {
+            if (gi < n) v = x[gi];
+        } else {
+            v = hist[gi + halo];
+        }
+        lds[fslot(e)] = v;
+    }
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < halo; j += kThreads) {
+            const long gi = n - halo + j;
+            hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+        }
+    }
+    __syncthreads();
+
+    T acc[kR], A[kR], B[kR];
+#pragma unroll
+    for (int r = 0; r < kR; r++) acc[r] = z;
+    const int base = tid * kR + halo;
+#pragma unroll
+    for (int j = 0; j < kR - 1; j++) B[j] = lds[fslot(base + 1 + j)];
+    B[kR - 1] = z;
+    const int nfull = L / kR;
+    const int rem = L - nfull * kR;
+    int kb = 0;
+    for (; kb + 2 <= nfull; kb += 2) {
+        fir_kblock<T, false>(acc, A, B, lds, base - kb * kR, h + kb * kR, 0);
+        fir_kblock<T, false>(acc, B, A, lds, base - (kb + 1) * kR, h + (kb + 1) * kR, 0);
+    }
+    if (kb < nfull) {
+        fir_kblock<T, false>(acc, A, B, lds, base - kb * kR, h + kb * kR, 0);
+        kb++;
+        if (rem) fir_kblock<T, true>(acc, B, A, lds, base - kb * kR, h + kb * kR, rem);
+    } else if (rem) {
+        fir_kblock<T, true>(acc, A, B, lds, base - kb * kR, h + kb * kR, rem);
+    }
+
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kR; r++) lds[fslot(tid * kR + r)] = vscale(acc[r], scale);
+    __syncthreads();
+    for (int e = tid; e < kTile; e += kThreads) {
+        const long gi = tile0 + e;
+        if (gi < n) y[gi] = lds[fslot(e)];
+    }
+}
+
+constexpr int kExactOut = 256;
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_fir_exact(const T* __restrict__ x, const T* __restrict__ hist,
+                                                        T* __restrict__ hist_out, long n,
+                                                        const float* __restrict__ hrev, int L, float scale,
+                                                        T* __restrict__ y)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* lds = reinterpret_cast<T*>(smem);
+    const long tile0 = (long)blockIdx.x * kExactOut;
+    const int halo = L - 1;
+    const int span = kExactOut + halo;
+    const int tid = threadIdx.x;
+    const T z = vzero(T());
+    for (int e = tid; e < span; e += kThreads) {
+        const long gi = tile0 - halo + e;
+        T v = z;
+        if (gi >= 0) {
+            if (gi < n) v = x[gi];
+        } else {
+            v = hist[gi + halo];
+        }
+        lds[e] = v;
+    }
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < halo; j += kThreads) {
+            const long gi = n - halo + j;
+            hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+        }
+    }
+    __syncthreads();
+    const long o = tile0 + tid;
+    if (o >= n) return;
+    T r = z;
+    for (int i = 0; i < L; i++) r = vmac(r, hrev[i], lds[tid + i]);
+    y[o] = vscale(r, scale);
+}
+
+template <typename T>
+__global__ void k_fir_hist_only(const T* __restrict__ x, const T* __restrict__ hist, T* __restrict__ hist_out,
+                                long n, int halo)
+{
+    for (int j = threadIdx.x; j < halo; j += blockDim.x) {
+        const long gi = n - halo + j;
+        hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+    }
+}
+
+size_t fast_lds_bytes(int L, size_t elem)
+{
+    const int span = kTile + L - 1;
+    return (size_t)(fslot(span - 1) + 1) * elem;
+}
+
+template <typename T>
+void fir_fast_t(const void* x, const void* hist, void* hist_out, size_t n, const float* taps, int L, float scale,
+                void* y, hipStream_t s)
+{
+    const size_t lds = fast_lds_bytes(L, sizeof(T));
+    if (lds > 64 * 1024)
+        LDSP_HIP(hipFuncSetAttribute((const void*)k_fir_fast<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+    const unsigned grid = (unsigned)((n + kTile - 1) / kTile);
+    hipLaunchKernelGGL(k_fir_fast<T>, dim3(grid), dim3(kThreads), lds, s, (const T*)x, (const T*)hist,
+                       (T*)hist_out, (long)n, taps, L, scale, (T*)y);
+    LDSP_HIP(hipGetLastError());
+}
+
+template <typename T>
+void fir_exact_t(const void* x, const void* hist, void* hist_out, size_t n, const float* taps, int L, float scale,
+                 void* y, hipStream_t s)
+{
+    const size_t lds = (size_t)(kExactOut + L - 1) * sizeof(T);
+    if (lds > 64 * 1024)
+        LDSP_HIP(hipFuncSetAttribute((const void*)k_fir_exact<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+    const unsigned grid = (unsigned)((n + kExactOut - 1) / kExactOut);
+    hipLaunchKernelGGL(k_fir_exact<T>, dim3(grid), dim3(kThreads), lds, s, (const T*)x, (const T*)hist,
+                       (T*)hist_out, (long)n, taps, L, scale, (T*)y);
+    LDSP_HIP(hipGetLastError());
+}
+
+template <typename T>
+void fir_hist_t(const void* x, const void* hist, void* hist_out, size_t n, int L, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_fir_hist_only<T>, dim3(1), dim3(256), 0, s, (const T*)x, (const T*)hist, (T*)hist_out,
+                       (long)n, L - 1);
+    LDSP_HIP(hipGetLastError());
+}
+
+} // namespace
+
+void fir_fast(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, const float* taps_pad, int L,
+              float scale, void* y, hipStream_t s)
+{
+    if (n == 0) {
+        if (L > 1) cplx ? fir_hist_t<float2>(x, hist, hist_out, n, L, s) : fir_hist_t<float>(x, hist, hist_out, n, L, s);
+        return;
+    }
+    if (cplx) fir_fast_t<float2>(x, hist, hist_out, n, taps_pad, L, scale, y, s);
+    else fir_fast_t<float>(x, hist, hist_out, n, taps_pad, L, scale, y, s);
+}
+
+void fir_exact(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, const float* taps_rev, int L,
+               float scale, void* y, hipStream_t s)
+{
+    if (n == 0) {
+        if (L > 1) cplx ? fir_hist_t<float2>(x, hist, hist_out, n, L, s) : fir_hist_t<float>(x, hist, hist_out, n, L, s);
+        return;
+    }
+    if (cplx) fir_exact_t<float2>(x, hist, hist_out, n, taps_rev, L, scale, y, s);
+    else fir_exact_t<float>(x, hist, hist_out, n, taps_rev, L, scale, y, s);
+}
+
+// ====================================================================== resampler
+namespace {
+
+__device__ __forceinline__ long resamp_j(uint64_t P0, uint64_t k, uint32_t step)
+{
+    // smallest input index j with P0 + k*step - j*2^24 <= 0xffffff
+    const long long num = (long long)(P0 + k * (uint64_t)step) - 0xffffffLL;
+    return num <= 0 ? 0 : (long)((num + 0xffffffLL) >> 24);
+}
+
+// complex taps (cccf): C99 complex product, sequential accumulation
+__device__ __forceinline__ void rs_mac(float2& r, float2 h, float2 v)
+{
+    r.x = r.x + (h.x * v.x - h.y * v.y);
+    r.y = r.y + (h.x * v.y + h.y * v.x);
+}
+
+template <bool CPLX>
+__global__ void __launch_bounds__(64) k_resamp(const void* __restrict__ xv_, const void* __restrict__ hist_,
+                                               void* __restrict__ hist_out_, long n, const float* __restrict__ sub,
+                                               ResampPlan p, void* __restrict__ y_)
+{
+    using T = typename std::conditional<CPLX, float2, float>::type;
+    const T* x = (const T*)xv_;
+    const T* hist = (const T*)hist_;
+    T* hist_out = (T*)hist_out_;
+    T* y = (T*)y_;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* lds = reinterpret_cast<T*>(smem);
+    const int tid = threadIdx.x;
+    const int halo = p.sub_len - 1;
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < halo; j += 64) {
+            const long gi = n - halo + j;
+            hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+        }
+    }
+    const long k0 = (long)blockIdx.x * p.KB;
+    const long k1 = min((long)p.K, k0 + p.KB);
+    if (k0 >= k1) return;
+    const long jlo = resamp_j(p.P0, k0, p.step) - halo;
+    const long jhi = resamp_j(p.P0, k1 - 1, p.step);
+    const int span = (int)(jhi - jlo + 1);
+    for (int e = tid; e < span; e += 64) {
+        const long gi = jlo + e;
+        T v;
+        if (gi >= 0) v = x[gi];
+        else v = hist[gi + halo];
+        lds[e] = v;
+    }
+    __syncthreads();
+    const long k = k0 + tid;
+    if (k >= k1) return;
+    const long j = resamp_j(p.P0, k, p.step);
+    const uint64_t ph = p.P0 + (uint64_t)k * p.step - ((uint64_t)j << 24);
+    const int b = (int)(ph >> p.bits_index);
+    const int off = (int)(j - halo - jlo);
+    if constexpr (CPLX) {
+        const float2* hb = reinterpret_cast<const float2*>(sub) + (size_t)b * p.sub_len;
+        float2 r = make_float2(0.0f, 0.0f);
+        for (int i = 0; i < p.sub_len; i++) rs_mac(r, hb[i], lds[off + i]);
+        y[k] = r;
+    } else {
+        const float* hb = sub + (size_t)b * p.sub_len;
+        float r = 0.0f;
+        for (int i = 0; i < p.sub_len; i++) r = r + hb[i] * lds[off + i];
+        y[k] = r;
+    }
+}
+
+} // namespace
+
+void resamp(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
+            const ResampPlan& p, void* y, hipStream_t s)
+{
+    const size_t elem = cplx ? 8 : 4;
+    const size_t lds = (size_t)p.span_max * elem;
+    const unsigned grid = (unsigned)std::max<size_t>(1, (p.K + p.KB - 1) / p.KB);
+    if (cplx) {
+        if (lds > 64 * 1024)
+            LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds));
+        hipLaunchKernelGGL(k_resamp<true>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
+    } else {
+        if (lds > 64 * 1024)
+            LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds));
+        hipLaunchKernelGGL(k_resamp<false>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
+    }
+    LDSP_HIP(hipGetLastError());
+}
+
+// ====================================================================== NCO
+namespace {
+
+__global__ void __launch_bounds__(256) k_nco_mix(const float2* __restrict__ x, float2* __restrict__ y, long n,
+                                                 uint32_t theta0, uint32_t dtheta, const float* __restrict__ table,
+                                                 int down)
+{
+    __shared__ float tab[1024];
+    for (int i = threadIdx.x; i < 1024; i += 256) tab[i] = table[i];
+    __syncthreads();
+    const long stride = (long)gridDim.x * 256;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const uint32_t th = theta0 + (uint32_t)((uint64_t)i * dtheta);
+        const uint32_t idx = ((th + (1u << 21)) >> 22) & 0x3ffu;
+        const float sn = tab[idx];
+        const float cs = tab[(idx + 256) & 0x3ffu];
+        const float2 v = x[i];
+        float2 o;
+        if (down) {   // x * conj(c + js): (a c - b (-s)) + j (a (-s) + b c)
+            o.x = v.x * cs - v.y * (-sn);
+            o.y = v.x * (-sn) + v.y * cs;
+        } else {      // x * (c + js)
+            o.x = v.x * cs - v.y * sn;
+            o.y = v.x * sn + v.y * cs;
+        }
+        y[i] = o;
+    }
+}
+
+// LIQUID_VCO: direct sin/cos of the fixed-point phase (not table based)
+__global__ void __launch_bounds__(256) k_vco_mix(const float2* __restrict__ x, float2* __restrict__ y, long n,
+                                                 uint32_t theta0, uint32_t dtheta, int down)
+{
+    const long stride = (long)gridDim.x * 256;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const uint32_t th = theta0 + (uint32_t)((uint64_t)i * dtheta);
+        const float a = (float)(6.283185307179586 * (double)(float)th / 4294967296.0);
+        float sn, cs;
+        sincosf(a, &sn, &cs);
+        const float2 v = x[i];
+        float2 o;
+        if (down) {
+            o.x = v.x * cs - v.y * (-sn);
+            o.y = v.x * (-sn) + v.y * cs;
+        } else {
+            o.x = v.x * cs - v.y * sn;
+            o.y = v.x * sn + v.y * cs;
+        }
+        y[i] = o;
+    }
+}
+
+} // namespace
+
+void nco_mix(const void* x, void* y, size_t n, uint32_t theta0, uint32_t dtheta, const float* table, bool down,
+             int type, hipStream_t s)
+{
+    if (n == 0) return;
+    const unsigned grid = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    if (type == 0)
+        hipLaunchKernelGGL(k_nco_mix, dim3(grid), dim3(256), 0, s, (const float2*)x, (float2*)y, (long)n, theta0,
+                           dtheta, table, (int)down);
+    else
+        hipLaunchKernelGGL(k_vco_mix, dim3(grid), dim3(256), 0, s, (const float2*)x, (float2*)y, (long)n, theta0,
+                           dtheta, (int)down);
+    LDSP_HIP(hipGetLastError());
+}
+
+} // namespace k
+} // namespace ldsp

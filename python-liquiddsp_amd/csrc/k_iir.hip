@@ -1,0 +1,540 @@
+// k_iir.hip -- IIR filter kernels for gfx950 (iirfilt_{rrrf,crcf}, reference
+// src/iirfilter.hpp:56,166,296,353 execute_block and :389 per-sample execute).
+//
+// The recursion is inherently sequential, so three evaluation strategies exist:
+//  iir_seq  : the float32 direct-form-II recursion exactly as liquid evaluates
+//             it (one lane per real component) -- bit-identical, slow.
+//  iir_scan : chunked linear scan in float64.  The cascade is a linear system
+//             s' = A s + B u; chunks of C samples run from a zero state (K1),
+//             a single workgroup propagates the chunk-boundary states with
+//             precomputed powers of A (K2), and every chunk re-runs from its
+//             true start state writing outputs (K3).  Error ~1e-12 relative,
+//             i.e. more accurate than liquid's float32 recursion.
+//  iir_spec : speculative exact chunks for fast-decaying filters (de-emphasis):
+//             each chunk starts W samples early from a zero state; because the
+//             filter forgets its state, the float32 trajectory coalesces
+//             bit-for-bit with the true one; a single-wave verifier compares
+//             every chunk's guessed start state with its predecessor's end state
+//             and re-runs the (rare) chunks that did not coalesce.
+#include "kernels.hpp"
+#include "ldsp_common.hpp"
+
+namespace ldsp {
+namespace k {
+
+namespace {
+
+constexpr int kMaxSos = 8;     // sections handled by the register-resident kernels
+
+// Loads in the verifier read words that another lane of the same wave may have
+// just rewritten; non-temporal loads are served from L2 (they bypass the CU's
+// vector L1), so they always see those writes.
+__device__ __forceinline__ float ldnt(const float* p) { return __builtin_nontemporal_load(p); }
+constexpr int kMaxTf = 17;     // TF coefficients (nv)
+
+// --------------------------------------------------------------- float32 step
+// iirfiltsos_execute_df2: v2=v1; v1=v0; v0 = x - a1 v1 - a2 v2; y = b0 v0 + b1 v1 + b2 v2
+struct SosF {
+    float b[kMaxSos][3], a[kMaxSos][3];
+    int nsos;
+};
+struct TfF {
+    float b[kMaxTf], a[kMaxTf];
+    int nb, na, nv;
+};
+
+__device__ __forceinline__ float sos_step(const SosF& c, float (&v)[kMaxSos][3], float x)
+{
+    float t = x;
+#pragma unroll
+    for (int s = 0; s < kMaxSos; s++) {
+        if (s < c.nsos) {
+            v[s][2] = v[s][1];
+            v[s][1] = v[s][0];
+            v[s][0] = t - c.a[s][1] * v[s][1] - c.a[s][2] * v[s][2];
+            t = c.b[s][0] * v[s][0] + c.b[s][1] * v[s][1] + c.b[s][2] * v[s][2];
+        }
+    }
+    return t;
+}
+
+// iirfilt_execute_norm: shift v; v0 = x - dot(a[1:], v[1:]); y = dot(b, v) (sequential dotprod)
+__device__ __forceinline__ float tf_step(const TfF& c, float (&v)[kMaxTf], float x)
+{
+#pragma unroll
+    for (int i = kMaxTf - 1; i > 0; i--)
+        if (i < c.nv) v[i] = v[i - 1];
+    float r = 0.0f;
+#pragma unroll
+    for (int i = 1; i < kMaxTf; i++)
+        if (i < c.na) r = r + c.a[i] * v[i];
+    v[0] = x - r;
+    float y = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kMaxTf; i++)
+        if (i < c.nb) y = y + c.b[i] * v[i];
+    return y;
+}
+
+__device__ void load_sos(SosF& c, const IirDesc& d)
+{
+    c.nsos = d.nsos;
+#pragma unroll
+    for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            c.b[s][k] = s < d.nsos ? d.b[3 * s + k] : 0.0f;
+            c.a[s][k] = s < d.nsos ? d.a[3 * s + k] : 0.0f;
+        }
+}
+__device__ void load_tf(TfF& c, const IirDesc& d)
+{
+    c.nb = d.nb;
+    c.na = d.na;
+    c.nv = d.nv;
+#pragma unroll
+    for (int i = 0; i < kMaxTf; i++) {
+        c.b[i] = i < d.nb ? d.b[i] : 0.0f;
+        c.a[i] = i < d.na ? d.a[i] : 0.0f;
+    }
+}
+
+// state layout in memory (float32): SOS [comp][nsos][3], TF [comp][nv]
+__device__ __forceinline__ int fstate_size(const IirDesc& d) { return d.sos ? 3 * d.nsos : d.nv; }
+
+// --------------------------------------------------------------- sequential
+__global__ void k_iir_seq(IirDesc d, const float* __restrict__ x, long n, int ncomp, float* __restrict__ state,
+                          float* __restrict__ y)
+{
+    const int c = threadIdx.x;
+    if (c >= ncomp) return;
+    float* st = state + c * fstate_size(d);
+    if (d.sos) {
+        SosF cf;
+        load_sos(cf, d);
+        float v[kMaxSos][3];
+#pragma unroll
+        for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) v[s][k] = s < d.nsos ? st[3 * s + k] : 0.0f;
+        for (long i = 0; i < n; i++) y[i * ncomp + c] = sos_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+        for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                if (s < d.nsos) st[3 * s + k] = v[s][k];
+    } else {
+        TfF cf;
+        load_tf(cf, d);
+        float v[kMaxTf];
+#pragma unroll
+        for (int i = 0; i < kMaxTf; i++) v[i] = i < d.nv ? st[i] : 0.0f;
+        for (long i = 0; i < n; i++) y[i * ncomp + c] = tf_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+        for (int i = 0; i < kMaxTf; i++)
+            if (i < d.nv) st[i] = v[i];
+    }
+}
+
+// --------------------------------------------------------------- speculative exact
+// scratch layout: [nchunks][2 (guess, end)][ncomp][fstate]  + flags
+__global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* __restrict__ x, long n, int ncomp,
+                                                        const float* __restrict__ state0, int C, int W, long nch,
+                                                        float* __restrict__ sc, float* __restrict__ y)
+{
+    const long ch = (long)blockIdx.x * 64 + threadIdx.x;
+    if (ch >= nch * ncomp) return;
+    const long chunk = ch / ncomp;
+    const int c = (int)(ch % ncomp);
+    const int fs = fstate_size(d);
+    const long s0 = chunk * C;
+    const long s1 = min(n, s0 + C);
+    long w0 = s0 - W;
+    float* guess = sc + ((chunk * 2 + 0) * ncomp + c) * fs;
+    float* endst = sc + ((chunk * 2 + 1) * ncomp + c) * fs;
+    const bool from_true = w0 <= 0;
+    if (from_true) w0 = 0;
+    if (d.sos) {
+        SosF cf;
+        load_sos(cf, d);
+        float v[kMaxSos][3];
+#pragma unroll
+        for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) v[s][k] = (from_true && s < d.nsos) ? state0[c * fs + 3 * s + k] : 0.0f;
+        for (long i = w0; i < s0; i++) (void)sos_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+        for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                if (s < d.nsos) guess[3 * s + k] = v[s][k];
+        for (long i = s0; i < s1; i++) y[i * ncomp + c] = sos_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+        for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                if (s < d.nsos) endst[3 * s + k] = v[s][k];
+    } else {
+        TfF cf;
+        load_tf(cf, d);
+        float v[kMaxTf];
+#pragma unroll
+        for (int i = 0; i < kMaxTf; i++) v[i] = (from_true && i < d.nv) ? state0[c * fs + i] : 0.0f;
+        for (long i = w0; i < s0; i++) (void)tf_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+        for (int i = 0; i < kMaxTf; i++)
+            if (i < d.nv) guess[i] = v[i];
+        for (long i = s0; i < s1; i++) y[i * ncomp + c] = tf_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+        for (int i = 0; i < kMaxTf; i++)
+            if (i < d.nv) endst[i] = v[i];
+    }
+}
+
+// Verifier: one wave walks the chunks in order.  Chunk k's outputs are exact
+// iff its guessed start state equals chunk k-1's (exact) end state bit for bit
+// (chunks whose warm-up reached the call start began from the true state).
+__global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* __restrict__ x, long n, int ncomp,
+                                                        int C, int W, long nch, float* __restrict__ sc,
+                                                        float* __restrict__ state, float* __restrict__ y)
+{
+    const int lane = threadIdx.x;
+    const int fs = fstate_size(d);
+    const int per = ncomp * fs;   // floats per (chunk, kind)
+    long k = 1;
+    while (k < nch) {
+        // lanes check chunks k .. k+63
+        const long kk = k + lane;
+        bool bad = false;
+        if (kk < nch && kk * C - W > 0) {
+            const float* g = sc + (kk * 2 + 0) * per;
+            const float* e = sc + ((kk - 1) * 2 + 1) * per;
+            for (int i = 0; i < per; i++) bad |= (__float_as_uint(ldnt(g + i)) != __float_as_uint(ldnt(e + i)));
+        }
+        const unsigned long long m = __ballot(bad);
+        if (m == 0) {
+            k += 64;
+            continue;
+        }
+        const long kb = k + __ffsll((long long)m) - 1;
+        // re-run chunk kb from chunk kb-1's end state (lane c handles component c)
+        if (lane < ncomp) {
+            const int c = lane;
+            const float* e = sc + ((kb - 1) * 2 + 1) * per + c * fs;
+            float* en = sc + (kb * 2 + 1) * per + c * fs;
+            float* gn = sc + (kb * 2 + 0) * per + c * fs;
+            const long s0 = kb * C, s1 = min(n, s0 + C);
+            if (d.sos) {
+                SosF cf;
+                load_sos(cf, d);
+                float v[kMaxSos][3];
+#pragma unroll
+                for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+                    for (int q = 0; q < 3; q++) v[s][q] = s < d.nsos ? ldnt(e + 3 * s + q) : 0.0f;
+                for (long i = s0; i < s1; i++) y[i * ncomp + c] = sos_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+                for (int s = 0; s < kMaxSos; s++)
+#pragma unroll
+                    for (int q = 0; q < 3; q++)
+                        if (s < d.nsos) en[3 * s + q] = v[s][q];
+            } else {
+                TfF cf;
+                load_tf(cf, d);
+                float v[kMaxTf];
+#pragma unroll
+                for (int i = 0; i < kMaxTf; i++) v[i] = i < d.nv ? ldnt(e + i) : 0.0f;
+                for (long i = s0; i < s1; i++) y[i * ncomp + c] = tf_step(cf, v, x[i * ncomp + c]);
+#pragma unroll
+                for (int i = 0; i < kMaxTf; i++)
+                    if (i < d.nv) en[i] = v[i];
+            }
+            for (int i = 0; i < fs; i++) gn[i] = ldnt(e + i);   // mark the chunk as verified
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        k = kb + 1;
+    }
+    // carried state = end state of the last chunk
+    for (int i = lane; i < per; i += 64) state[i] = ldnt(sc + ((nch - 1) * 2 + 1) * per + i);
+}
+
+// --------------------------------------------------------------- float64 scan
+// double state vector per component: SOS [2s, 2s+1] = (v0, v1) of section s
+// (the values that become v1, v2 at the next step); TF [i] = v[i], i < nv - 1.
+constexpr int kMaxD = 16;
+
+struct CoefD {
+    double b[kMaxD + 1], a[kMaxD + 1];
+};
+
+__device__ __forceinline__ void load_coefd(CoefD& c, const IirDesc& d)
+{
+    const int nbv = d.sos ? 3 * d.nsos : d.nb;
+    const int nav = d.sos ? 3 * d.nsos : d.na;
+#pragma unroll
+    for (int i = 0; i <= kMaxD; i++) {
+        c.b[i] = i < nbv ? (double)d.b[i] : 0.0;
+        c.a[i] = i < nav ? (double)d.a[i] : 0.0;
+    }
+}
+
+// SOS coefficients for section s live at [3s..3s+2]; kMaxD/2 = 8 sections -> 24
+// entries, so SOS uses a wider table.
+struct SosD {
+    double b[kMaxD / 2][3], a[kMaxD / 2][3];
+};
+__device__ __forceinline__ void load_sosd(SosD& c, const IirDesc& d)
+{
+#pragma unroll
+    for (int s = 0; s < kMaxD / 2; s++)
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            c.b[s][q] = s < d.nsos ? (double)d.b[3 * s + q] : 0.0;
+            c.a[s][q] = s < d.nsos ? (double)d.a[3 * s + q] : 0.0;
+        }
+}
+
+__device__ __forceinline__ double sos_step_d(const SosD& c, int nsos, double (&v)[kMaxD], double x)
+{
+    double t = x;
+#pragma unroll
+    for (int s = 0; s < kMaxD / 2; s++) {
+        if (s < nsos) {
+            const double v1 = v[2 * s], v2 = v[2 * s + 1];
+            const double v0 = fma(-c.a[s][2], v2, fma(-c.a[s][1], v1, t));
+            t = fma(c.b[s][2], v2, fma(c.b[s][1], v1, c.b[s][0] * v0));
+            v[2 * s + 1] = v1;
+            v[2 * s] = v0;
+        }
+    }
+    return t;
+}
+
+__device__ __forceinline__ double tf_step_d(const CoefD& c, int nb, int na, double (&v)[kMaxD], double x)
+{
+    double r = x;
+#pragma unroll
+    for (int i = 1; i <= kMaxD; i++)
+        if (i < na) r = fma(-c.a[i], v[i - 1], r);
+    double y = c.b[0] * r;
+#pragma unroll
+    for (int i = 1; i <= kMaxD; i++)
+        if (i < nb) y = fma(c.b[i], v[i - 1], y);
+#pragma unroll
+    for (int i = kMaxD - 1; i > 0; i--) v[i] = v[i - 1];
+    v[0] = r;
+    return y;
+}
+
+template <bool WRITE>
+__device__ __forceinline__ void run_chunk_d(const IirDesc& d, const float* __restrict__ x, long s0, long s1,
+                                            int ncomp, int c, double (&v)[kMaxD], float* __restrict__ y)
+{
+    if (d.sos) {
+        SosD cf;
+        load_sosd(cf, d);
+        const int ns = d.nsos;
+        for (long i = s0; i < s1; i++) {
+            const double o = sos_step_d(cf, ns, v, (double)x[i * ncomp + c]);
+            if (WRITE) y[i * ncomp + c] = (float)o;
+        }
+    } else {
+        CoefD cf;
+        load_coefd(cf, d);
+        const int nb = d.nb, na = d.na;
+        for (long i = s0; i < s1; i++) {
+            const double o = tf_step_d(cf, nb, na, v, (double)x[i * ncomp + c]);
+            if (WRITE) y[i * ncomp + c] = (float)o;
+        }
+    }
+}
+
+// K1: end state of each chunk from a zero start (per component)
+__global__ void __launch_bounds__(256) k_iir_scan_local(IirDesc d, const float* __restrict__ x, long n, int ncomp,
+                                                        int C, long nch, double* __restrict__ Lout)
+{
+    const long chunk = (long)blockIdx.x * 256 + threadIdx.x;
+    if (chunk >= nch) return;
+    const long s0 = chunk * C, s1 = min(n, s0 + C);
+    for (int c = 0; c < ncomp; c++) {
+        double v[kMaxD];
+#pragma unroll
+        for (int i = 0; i < kMaxD; i++) v[i] = 0.0;
+        run_chunk_d<false>(d, x, s0, s1, ncomp, c, v, nullptr);
+        double* o = Lout + (chunk * ncomp + c) * d.D;
+#pragma unroll
+        for (int i = 0; i < kMaxD; i++)
+            if (i < d.D) o[i] = v[i];
+    }
+}
+
+// out += M in, D x D row-major, all in registers (D is a template constant)
+template <int D>
+__device__ __forceinline__ void matvec_acc(const double* __restrict__ M, const double (&in)[D], double (&out)[D])
+{
+#pragma unroll
+    for (int r = 0; r < D; r++) {
+        double acc = out[r];
+#pragma unroll
+        for (int q = 0; q < D; q++) acc = fma(M[r * D + q], in[q], acc);
+        out[r] = acc;
+    }
+}
+
+// K2: one workgroup of 1024 threads; thread t owns chunks [t G, (t+1) G).
+// Writes carry[c] = start state of chunk c (per component).
+template <int D>
+__global__ void __launch_bounds__(1024) k_iir_scan_carry(int ncomp, long nch, int G, int levels,
+                                                         const double* __restrict__ AC,
+                                                         const double* __restrict__ AG,
+                                                         const double* __restrict__ state0,
+                                                         const double* __restrict__ Lc, double* __restrict__ carry)
+{
+    extern __shared__ __attribute__((aligned(16))) double sh[];   // [1024][D]
+    const int t = threadIdx.x;
+    const long c0 = (long)t * G;
+    const long c1 = min(nch, c0 + G);
+    for (int comp = 0; comp < ncomp; comp++) {
+        double P[D], Q[D];
+#pragma unroll
+        for (int i = 0; i < D; i++) P[i] = 0.0;
+        for (long c = c0; c < c1; c++) {
+#pragma unroll
+            for (int i = 0; i < D; i++) Q[i] = Lc[(c * ncomp + comp) * D + i];
+            matvec_acc<D>(AC, P, Q);
+#pragma unroll
+            for (int i = 0; i < D; i++) P[i] = Q[i];
+        }
+        __syncthreads();
+        if (t + 1 < 1024)
+#pragma unroll
+            for (int i = 0; i < D; i++) sh[(t + 1) * D + i] = P[i];
+        if (t == 0)
+#pragma unroll
+            for (int i = 0; i < D; i++) sh[i] = state0[comp * D + i];
+        __syncthreads();
+        // inclusive Hillis-Steele scan: I_t = M I_{t-1} + e_t with M = A^{C G}
+        for (int l = 0; l < levels; l++) {
+            const int dd = 1 << l;
+            double mine[D], other[D];
+#pragma unroll
+            for (int i = 0; i < D; i++) {
+                mine[i] = sh[t * D + i];
+                other[i] = t >= dd ? sh[(t - dd) * D + i] : 0.0;
+            }
+            __syncthreads();
+            if (t >= dd) {
+                matvec_acc<D>(AG + (size_t)l * D * D, other, mine);
+#pragma unroll
+                for (int i = 0; i < D; i++) sh[t * D + i] = mine[i];
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < D; i++) P[i] = sh[t * D + i];
+        for (long c = c0; c < c1; c++) {
+#pragma unroll
+            for (int i = 0; i < D; i++) {
+                carry[(c * ncomp + comp) * D + i] = P[i];
+                Q[i] = Lc[(c * ncomp + comp) * D + i];
+            }
+            matvec_acc<D>(AC, P, Q);
+#pragma unroll
+            for (int i = 0; i < D; i++) P[i] = Q[i];
+        }
+    }
+}
+
+// K3: every chunk from its true start state, outputs in float; the last chunk
+// writes the carried state.
+__global__ void __launch_bounds__(256) k_iir_scan_final(IirDesc d, const float* __restrict__ x, long n, int ncomp,
+                                                        int C, long nch, const double* __restrict__ carry,
+                                                        double* __restrict__ state64, float* __restrict__ y)
+{
+    const long chunk = (long)blockIdx.x * 256 + threadIdx.x;
+    if (chunk >= nch) return;
+    const long s0 = chunk * C, s1 = min(n, s0 + C);
+    for (int c = 0; c < ncomp; c++) {
+        double v[kMaxD];
+        const double* in = carry + (chunk * ncomp + c) * d.D;
+#pragma unroll
+        for (int i = 0; i < kMaxD; i++) v[i] = i < d.D ? in[i] : 0.0;
+        run_chunk_d<true>(d, x, s0, s1, ncomp, c, v, y);
+        if (chunk == nch - 1)
+#pragma unroll
+            for (int i = 0; i < kMaxD; i++)
+                if (i < d.D) state64[c * d.D + i] = v[i];
+    }
+}
+
+template <int D>
+void launch_carry(int ncomp, const IirScanPlan& p, const double* state64, hipStream_t s)
+{
+    const size_t lds = (size_t)1024 * D * sizeof(double);
+    if (lds > 64 * 1024)
+        LDSP_HIP(hipFuncSetAttribute((const void*)k_iir_scan_carry<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+    hipLaunchKernelGGL(k_iir_scan_carry<D>, dim3(1), dim3(1024), lds, s, ncomp, p.nchunks, p.G, p.levels, p.AC,
+                       p.AG, state64, p.local, p.carry);
+    LDSP_HIP(hipGetLastError());
+}
+
+} // namespace
+
+void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s)
+{
+    if (n == 0) return;
+    LDSP_REQUIRE(d.sos ? d.nsos <= kMaxSos : d.nv <= kMaxTf, "iir: filter order too high for the GPU kernels");
+    hipLaunchKernelGGL(k_iir_seq, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, cplx ? 2 : 1, state,
+                       (float*)y);
+    LDSP_HIP(hipGetLastError());
+}
+
+void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, const SpecPlan& p, void* y,
+              hipStream_t s)
+{
+    if (n == 0) return;
+    const int ncomp = cplx ? 2 : 1;
+    const long work = p.nchunks * ncomp;
+    hipLaunchKernelGGL(k_iir_spec_chunks, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, s, d, (const float*)x,
+                       (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks, (float*)p.scratch, (float*)y);
+    LDSP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_iir_spec_verify, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, ncomp, p.C, p.W,
+                       p.nchunks, (float*)p.scratch, state, (float*)y);
+    LDSP_HIP(hipGetLastError());
+}
+
+void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* state64, const IirScanPlan& p, void* y,
+              hipStream_t s)
+{
+    if (n == 0) return;
+    LDSP_REQUIRE(d.D >= 1 && d.D <= kMaxD, "iir: state dimension too large for the scan kernels");
+    const int ncomp = cplx ? 2 : 1;
+    const unsigned g = (unsigned)((p.nchunks + 255) / 256);
+    hipLaunchKernelGGL(k_iir_scan_local, dim3(g), dim3(256), 0, s, d, (const float*)x, (long)n, ncomp, p.C,
+                       p.nchunks, p.local);
+    LDSP_HIP(hipGetLastError());
+    switch (d.D) {
+    case 1: launch_carry<1>(ncomp, p, state64, s); break;
+    case 2: launch_carry<2>(ncomp, p, state64, s); break;
+    case 3: launch_carry<3>(ncomp, p, state64, s); break;
+    case 4: launch_carry<4>(ncomp, p, state64, s); break;
+    case 5: launch_carry<5>(ncomp, p, state64, s); break;
+    case 6: launch_carry<6>(ncomp, p, state64, s); break;
+    case 7: launch_carry<7>(ncomp, p, state64, s); break;
+    case 8: launch_carry<8>(ncomp, p, state64, s); break;
+    case 10: launch_carry<10>(ncomp, p, state64, s); break;
+    case 12: launch_carry<12>(ncomp, p, state64, s); break;
+    case 14: launch_carry<14>(ncomp, p, state64, s); break;
+    case 16: launch_carry<16>(ncomp, p, state64, s); break;
+    default:
+        throw Error(LDSP_EUNSUP, "iir: unsupported state dimension for the scan kernels");
+    }
+    hipLaunchKernelGGL(k_iir_scan_final, dim3(g), dim3(256), 0, s, d, (const float*)x, (long)n, ncomp, p.C,
+                       p.nchunks, p.carry, state64, (float*)y);
+    LDSP_HIP(hipGetLastError());
+}
+
+} // namespace k
+} // namespace ldsp

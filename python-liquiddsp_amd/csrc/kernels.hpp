@@ -1,0 +1,113 @@
+// kernels.hpp -- host launchers for the gfx950 kernels of libldsp.
+// All pointers are device pointers; every launcher only enqueues on `s`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace ldsp {
+namespace k {
+
+// ------------------------------------------------------------------ FIR
+// y[i] = scale * sum_{k<L} h[k] xv[i-k], xv[j<0] = hist[j + L - 1]; writes the
+// new history (last L-1 samples of xv) to hist_out.  taps_pad has
+// ceil(L/16)*16 floats (zero padded).  fast: register-blocked FMA kernel;
+// exact: liquid dotprod order (oldest sample first, separate mul and add).
+constexpr int kFirMaxTaps = 8192;
+void fir_fast(bool cplx, const void* x, const void* hist, void* hist_out, size_t n,
+              const float* taps_pad, int L, float scale, void* y, hipStream_t s);
+void fir_exact(bool cplx, const void* x, const void* hist, void* hist_out, size_t n,
+               const float* taps_rev, int L, float scale, void* y, hipStream_t s);
+// history update only (n == 0 calls skip the kernels)
+
+// ------------------------------------------------------------------ resampler
+struct ResampPlan {
+    uint64_t P0;          // phase at call start (resamp "phase", < 2^24 + step)
+    uint32_t step;        // round(2^24 / rate)
+    int bits_index;       // 24 - log2(npfb)
+    int sub_len;          // taps per branch (2m)
+    int npfb;
+    size_t K;             // outputs of this call
+    int KB;               // outputs per workgroup
+    int span_max;         // LDS samples per workgroup
+};
+// sub: [npfb][sub_len] branch taps reversed (cplx: complex64 with imag, rrrf: float)
+void resamp(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
+            const ResampPlan& p, void* y, hipStream_t s);
+
+// ------------------------------------------------------------------ NCO
+void nco_mix(const void* x, void* y, size_t n, uint32_t theta0, uint32_t dtheta, const float* table,
+             bool down, int type, hipStream_t s);
+
+// ------------------------------------------------------------------ IIR
+// Structure of one IIR filter for the kernels.  SOS: nsos sections b[3],a[3]
+// (a0 == 1); TF: nb, na coefficients (a0 == 1), nv = max(nb, na).
+constexpr int kIirMaxState = 16;
+struct IirDesc {
+    int sos;              // 1 SOS cascade, 0 TF
+    int nsos;
+    int nb, na, nv;
+    int D;                // state dimension (SOS: 2 nsos, TF: nv - 1)
+    const float* b;       // device coefficients
+    const float* a;
+};
+// Sequential float32 evaluation (bit-exact with the liquid recursion).
+// state: float[2][3*nsos] (SOS) or float[2][nv] (TF); cplx -> 2 components.
+void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
+// Float64 chunked linear scan.  state64: double[2][D] (the DF-II delay line in
+// the layout used by the scan); Apow: double[D*D] matrices: [0] = A^C,
+// [1 + l] = A^{C G 2^l} prepared by the host (see IirScanPlan).
+struct IirScanPlan {
+    int C;                // samples per chunk
+    long nchunks;
+    int G;                // chunks per scan thread (1024 scan threads)
+    int levels;           // 10 = log2(1024)
+    const double* AC;     // A^C           [D*D]
+    const double* AG;     // A^{C*G*2^l}    [levels][D*D]
+    double* local;        // [nchunks][ncomp][D] scratch: chunk end state from zero
+    double* carry;        // [nchunks][ncomp][D] scratch: chunk start state
+};
+void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* state64, const IirScanPlan& p,
+              void* y, hipStream_t s);
+// Speculative exact evaluation for fast-decaying filters: chunks start from a
+// zero state W samples early; a verifier re-runs any chunk whose guessed
+// start state differs bit-wise from its predecessor's end state.
+struct SpecPlan {
+    int C;                // samples per chunk
+    int W;                // warm-up samples
+    long nchunks;
+    void* scratch;        // device scratch (states: start-guess and end per chunk)
+};
+void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, const SpecPlan& p, void* y,
+              hipStream_t s);
+
+// ------------------------------------------------------------------ AGC
+struct AgcState {         // device-resident agc_crcf state
+    float g, y2p, alpha, scale;
+    int locked, mode;
+    unsigned int timer, timeout;
+    float threshold;
+    int pad[3];
+};
+void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hipStream_t s);
+void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
+              hipStream_t s);
+
+// ------------------------------------------------------------------ AmpModem
+struct AmpState {         // device-resident PLL state
+    uint32_t theta, dtheta;
+    float alpha, beta;
+};
+// x0 = lowpass(x) (precomputed), x1 = delay_m(x) via hist (m samples); writes
+// m = Re(v1)/mod (carrier) or the final output (Costas) to y.  scratch (of
+// pll_scratch_bytes(n)) enables the chunk-parallel exact path (k_pll.hip).
+size_t pll_scratch_bytes(size_t n);
+void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_out, int m, size_t n,
+                  AmpState* st, const float* table, float mod_index, int costas, float* y, void* scratch,
+                  hipStream_t s);
+
+// ------------------------------------------------------------------ debug
+void math_eval(int fn, const float* a, const float* b, float* y, size_t n, hipStream_t s);
+
+} // namespace k
+} // namespace ldsp

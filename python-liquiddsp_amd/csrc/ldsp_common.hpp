@@ -1,0 +1,81 @@
+// ldsp_common.hpp -- shared host-side plumbing for libldsp: error reporting,
+// HIP checks, grow-only device buffers, stream selection.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/ldsp.h"
+
+namespace ldsp {
+
+// Error carried from the implementation to the C ABI boundary (-> ldsp_last_error()).
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& msg);
+
+#define LDSP_HIP(call)                                                                     \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            throw ::ldsp::Error(LDSP_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define LDSP_REQUIRE(cond, msg)                                                            \
+    do {                                                                                   \
+        if (!(cond)) throw ::ldsp::Error(LDSP_EINVAL, (msg));                              \
+    } while (0)
+
+// Grow-only device allocation owned by one object (allocation happens lazily,
+// outside any timed/captured region once warmed up).
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int device = -1;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) {
+            int cur = 0;
+            if (hipGetDevice(&cur) == hipSuccess && cur != device) (void)hipSetDevice(device);
+            (void)hipFree(p);
+            if (cur != device) (void)hipSetDevice(cur);
+        }
+        p = nullptr;
+        cap = 0;
+    }
+    void* ensure(size_t bytes, int dev) {
+        if (bytes <= cap && p) return p;
+        release();
+        device = dev;
+        LDSP_HIP(hipMalloc(&p, bytes ? bytes : 16));
+        cap = bytes;
+        return p;
+    }
+    template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Select the device an object lives on and make it current for the call.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        LDSP_HIP(hipGetDevice(&prev));
+        if (prev != dev) LDSP_HIP(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur;
+        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int current_device();                       // throws LDSP_EHIP when no GPU is present
+hipStream_t library_stream(int device);     // per-device non-blocking stream for host-memory calls
+
+} // namespace ldsp

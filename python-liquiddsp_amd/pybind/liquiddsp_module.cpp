@@ -1,0 +1,827 @@
+// liquiddsp_module.cpp -- the pybind11 module `liquiddsp`: same class names,
+// constructor keywords, defaults, properties and __call__ semantics as the
+// reference module (colbyAtCRI/python-liquiddsp src/wrapper.cpp:10-273), bound
+// to the MI355X C ABI (include/ldsp.h) instead of liquid-dsp.
+//
+// Array handling (reference src/liquiddsp.hpp:16-20 array_to_ptr):
+//  * numpy / lists / other dtypes are force-cast to contiguous complex64 /
+//    float32 (the reference read strided views as if contiguous; this module
+//    copies them), staged to the GPU, processed, and a new
+//    numpy array is returned.
+//  * a torch tensor on a ROCm device is processed in place on the device,
+//    enqueued on torch's current stream, and a new device tensor is returned
+//    (no host round trip; this is how chains stay resident in HBM).
+// The GIL is released while a call waits for the GPU.
+#include <pybind11/complex.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/ldsp.h"
+
+namespace py = pybind11;
+using cf = std::complex<float>;
+
+namespace {
+
+// ------------------------------------------------------------------ errors
+void check(int rc)
+{
+    if (rc == LDSP_OK) return;
+    const std::string msg = ldsp_last_error();
+    if (rc == LDSP_EINVAL || rc == LDSP_ERANGE) throw py::value_error(msg);
+    if (rc == LDSP_EUNSUP) {
+        PyErr_SetString(PyExc_NotImplementedError, msg.c_str());
+        throw py::error_already_set();
+    }
+    throw std::runtime_error(msg);
+}
+
+// ------------------------------------------------------------------ torch interop
+py::object& torch_mod()
+{
+    static py::object t = py::module_::import("torch");
+    return t;
+}
+
+bool is_device_tensor(const py::handle& o)
+{
+    if (!py::hasattr(o, "is_cuda") || !py::hasattr(o, "data_ptr")) return false;
+    return o.attr("is_cuda").cast<bool>();
+}
+
+struct DevIn {
+    py::object t;       // contiguous tensor kept alive for the call
+    void* ptr;
+    size_t n;
+    void* stream;
+    py::object device;
+};
+
+DevIn dev_in(const py::handle& x, bool cplx)
+{
+    py::object& torch = torch_mod();
+    py::object want = cplx ? torch.attr("complex64") : torch.attr("float32");
+    py::object t = py::reinterpret_borrow<py::object>(x);
+    if (!py::object(t.attr("dtype")).equal(want)) t = t.attr("to")(want);
+    t = t.attr("reshape")(-1).attr("contiguous")();
+    DevIn d;
+    d.device = t.attr("device");
+    d.ptr = reinterpret_cast<void*>(t.attr("data_ptr")().cast<uintptr_t>());
+    d.n = t.attr("numel")().cast<size_t>();
+    d.stream = reinterpret_cast<void*>(
+        torch.attr("cuda").attr("current_stream")(d.device).attr("cuda_stream").cast<uintptr_t>());
+    d.t = t;
+    return d;
+}
+
+py::object dev_empty(size_t n, bool cplx, const py::object& device)
+{
+    py::object& torch = torch_mod();
+    py::dict kw;
+    kw["dtype"] = cplx ? torch.attr("complex64") : torch.attr("float32");
+    kw["device"] = device;
+    return torch.attr("empty")(py::int_(n), **kw);
+}
+
+void* tptr(const py::object& t) { return reinterpret_cast<void*>(t.attr("data_ptr")().cast<uintptr_t>()); }
+
+using carr = py::array_t<cf, py::array::c_style | py::array::forcecast>;
+using farr = py::array_t<float, py::array::c_style | py::array::forcecast>;
+
+// Same-length stage (FIR / IIR / NCO / AGC): in -> out of the given kinds
+template <typename F>
+py::object run_same(const py::handle& x, bool cin, bool cout, F&& exec)
+{
+    if (is_device_tensor(x)) {
+        DevIn d = dev_in(x, cin);
+        py::object out = dev_empty(d.n, cout, d.device);
+        check(exec(d.ptr, d.n, tptr(out), LDSP_MEM_DEVICE, d.stream));
+        return out;
+    }
+    if (cin) {
+        carr a = carr::ensure(x);
+        if (!a) throw py::error_already_set();
+        const size_t n = (size_t)a.size();
+        py::object out = cout ? py::object(py::array_t<cf>(n)) : py::object(py::array_t<float>(n));
+        void* yp = py::array(out).mutable_data();
+        int rc;
+        {
+            py::gil_scoped_release rel;
+            rc = exec((const void*)a.data(), n, yp, LDSP_MEM_HOST, nullptr);
+        }
+        check(rc);
+        return out;
+    }
+    farr a = farr::ensure(x);
+    if (!a) throw py::error_already_set();
+    const size_t n = (size_t)a.size();
+    py::object out = cout ? py::object(py::array_t<cf>(n)) : py::object(py::array_t<float>(n));
+    void* yp = py::array(out).mutable_data();
+    int rc;
+    {
+        py::gil_scoped_release rel;
+        rc = exec((const void*)a.data(), n, yp, LDSP_MEM_HOST, nullptr);
+    }
+    check(rc);
+    return out;
+}
+
+std::vector<float> to_fvec(const py::handle& h)
+{
+    farr a = farr::ensure(h);
+    if (!a) throw py::error_already_set();
+    return std::vector<float>(a.data(), a.data() + a.size());
+}
+
+// ------------------------------------------------------------------ FIR
+struct FIR {
+    ldsp_firfilt_t q = nullptr;
+    bool cplx = false;
+    FIR() = default;
+    FIR(const FIR&) = delete;
+    ~FIR() { if (q) ldsp_firfilt_destroy(q); }
+    cf freqresponse(float f)
+    {
+        float re, im;
+        check(ldsp_firfilt_freqresponse(q, f, &re, &im));
+        return cf(re, im);
+    }
+    py::object call(const py::handle& x)
+    {
+        return run_same(x, cplx, cplx, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            return ldsp_firfilt_execute(q, xi, n, yo, mem, s);
+        });
+    }
+    void reset() { check(ldsp_firfilt_reset(q)); }
+    bool get_exact()
+    {
+        return exact_;
+    }
+    void set_exact(bool e)
+    {
+        check(ldsp_firfilt_set_mode(q, e ? LDSP_MODE_EXACT : LDSP_MODE_FAST));
+        exact_ = e;
+    }
+    py::array_t<float> taps()
+    {
+        unsigned n;
+        check(ldsp_firfilt_get_length(q, &n));
+        py::array_t<float> h(n);
+        check(ldsp_firfilt_get_taps(q, h.mutable_data()));
+        return h;
+    }
+    float get_scale()
+    {
+        float s;
+        check(ldsp_firfilt_get_scale(q, &s));
+        return s;
+    }
+    bool exact_ = false;
+};
+
+// RealFIRFilter (firfilter.hpp:5-36)
+struct RealFIRFilter : FIR {
+    RealFIRFilter() = default;
+    explicit RealFIRFilter(const py::handle& h)
+    {
+        std::vector<float> v = to_fvec(h);
+        check(ldsp_firfilt_create(v.data(), (unsigned)v.size(), 0, &q));
+    }
+};
+// ComplexFIRFilter: new class (firfilt_crcf semantics of demod.hpp:105,135-136)
+struct ComplexFIRFilter : FIR {
+    explicit ComplexFIRFilter(const py::handle& h)
+    {
+        cplx = true;
+        std::vector<float> v = to_fvec(h);
+        check(ldsp_firfilt_create(v.data(), (unsigned)v.size(), 1, &q));
+    }
+};
+// RealDCBlocker (firfilter.hpp:38-50)
+struct RealDCBlocker : FIR {
+    RealDCBlocker(int m, float as)
+    {
+        if (m < 1) throw py::value_error("RealDCBlocker: slen must be >= 1");
+        check(ldsp_firfilt_create_dc_blocker((unsigned)m, as, 0, &q));
+    }
+};
+// RealKaiserBessel (firfilter.hpp:52-66): unit DC gain via set_scale(1/|H(0)|)
+struct RealKaiserBessel : FIR {
+    RealKaiserBessel(int flen, float fc, float as, float offset)
+    {
+        if (flen < 1) throw py::value_error("RealKaiserBessel: flen must be >= 1");
+        check(ldsp_firfilt_create_kaiser((unsigned)flen, fc, as, offset, 0, &q));
+        const cf res0 = freqresponse(0.0f);
+        check(ldsp_firfilt_set_scale(q, (float)(1.0 / (double)std::abs(res0))));
+    }
+};
+
+// ------------------------------------------------------------------ resamplers
+struct Resampler {
+    ldsp_resamp_t q = nullptr;
+    bool cplx;
+    float rate_, fc_, as_;
+    int m_, npfb_;
+    Resampler(float r, int d, float fc, float sbsp, int nf, bool c) : cplx(c), rate_(r), fc_(fc), as_(sbsp), m_(d), npfb_(nf)
+    {
+        if (d < 1) throw py::value_error("resampler: len must be >= 1");
+        if (nf < 1) throw py::value_error("resampler: nfilter must be >= 1");
+        check(ldsp_resamp_create(r, (unsigned)d, fc, sbsp, (unsigned)nf, c ? 1 : 0, &q));
+    }
+    Resampler(const Resampler&) = delete;
+    ~Resampler() { if (q) ldsp_resamp_destroy(q); }
+    void reset() { check(ldsp_resamp_reset(q)); }
+    float get_rate() { return rate_; }
+    void set_rate(float r)
+    {
+        check(ldsp_resamp_set_rate(q, r));
+        rate_ = r;
+    }
+    void print()
+    {
+        unsigned npfb, sub;
+        uint32_t step, phase;
+        check(ldsp_resamp_get_info(q, &npfb, &step, &phase, &sub));
+        py::print(py::str("<liquid.resamp_{}, rate={}, m={}, as={:.3f}, fc={:.3f}, npfb={}>")
+                      .format(cplx ? "cccf" : "rrrf", rate_, m_, as_, fc_, npfb));
+    }
+    py::object call(const py::handle& x)
+    {
+        if (is_device_tensor(x)) {
+            DevIn d = dev_in(x, cplx);
+            size_t nout = 0;
+            check(ldsp_resamp_num_outputs(q, d.n, &nout));
+            py::object out = dev_empty(nout, cplx, d.device);
+            size_t nw = 0;
+            check(ldsp_resamp_execute(q, d.ptr, d.n, tptr(out), nout, &nw, LDSP_MEM_DEVICE, d.stream));
+            return out;
+        }
+        py::array a = cplx ? py::array(carr::ensure(x)) : py::array(farr::ensure(x));
+        if (!a) throw py::error_already_set();
+        const size_t n = (size_t)a.size();
+        size_t nout = 0;
+        check(ldsp_resamp_num_outputs(q, n, &nout));
+        py::array out = cplx ? py::array(py::array_t<cf>(nout)) : py::array(py::array_t<float>(nout));
+        void* yp = out.mutable_data();
+        const void* xp = a.data();
+        size_t nw = 0;
+        int rc;
+        {
+            py::gil_scoped_release rel;
+            rc = ldsp_resamp_execute(q, xp, n, yp, nout, &nw, LDSP_MEM_HOST, nullptr);
+        }
+        check(rc);
+        return out;
+    }
+};
+
+// ------------------------------------------------------------------ IIR
+// filter_type_map / band_type_map (iirfilter.hpp:5-20)
+const std::map<std::string, int> kFilterTypes = {{"butter", 0}, {"cheby1", 1}, {"cheby2", 2}, {"ellip", 3}, {"bessel", 4}};
+const std::map<std::string, int> kBandTypes = {{"lowpass", 0}, {"highpass", 1}, {"bandpass", 2}, {"bandstop", 3}};
+
+int ftype_of(const std::string& s)
+{
+    auto it = kFilterTypes.find(s);
+    return it == kFilterTypes.end() ? 0 : it->second;
+}
+
+struct IIR {
+    ldsp_iirfilt_t q = nullptr;
+    bool cplx = true;
+    bool exact_ = false;
+    IIR() = default;
+    IIR(const IIR&) = delete;
+    ~IIR() { if (q) ldsp_iirfilt_destroy(q); }
+    void reset() { check(ldsp_iirfilt_reset(q)); }
+    cf freqresponse(float f)
+    {
+        float re, im;
+        check(ldsp_iirfilt_freqresponse(q, f, &re, &im));
+        return cf(re, im);
+    }
+    py::object call(const py::handle& x)
+    {
+        return run_same(x, cplx, cplx, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            return ldsp_iirfilt_execute(q, xi, n, yo, mem, s);
+        });
+    }
+    bool get_exact() { return exact_; }
+    void set_exact(bool e)
+    {
+        check(ldsp_iirfilt_set_mode(q, e ? LDSP_MODE_EXACT : LDSP_MODE_FAST));
+        exact_ = e;
+    }
+    py::tuple sos()
+    {
+        unsigned n;
+        check(ldsp_iirfilt_get_nsos(q, &n));
+        py::array_t<float> B({(py::ssize_t)n, (py::ssize_t)3}), A({(py::ssize_t)n, (py::ssize_t)3});
+        check(ldsp_iirfilt_get_sos(q, B.mutable_data(), A.mutable_data()));
+        return py::make_tuple(B, A);
+    }
+    void print()
+    {
+        unsigned n = 0;
+        check(ldsp_iirfilt_get_nsos(q, &n));
+        if (n == 0) {
+            py::print(py::str("<liquid.iirfilt_{}, type=tf>").format(cplx ? "crcf" : "rrrf"));
+            return;
+        }
+        std::vector<float> B(3 * n), A(3 * n);
+        check(ldsp_iirfilt_get_sos(q, B.data(), A.data()));
+        py::print(py::str("<liquid.iirfilt_{}, type=sos, order={}>").format(cplx ? "crcf" : "rrrf", 2 * n));
+        for (unsigned s = 0; s < n; s++)
+            py::print(py::str("  B[{}] = [{:12.8f} {:12.8f} {:12.8f}]  A[{}] = [{:12.8f} {:12.8f} {:12.8f}]")
+                          .format(s, B[3 * s], B[3 * s + 1], B[3 * s + 2], s, A[3 * s], A[3 * s + 1], A[3 * s + 2]));
+    }
+};
+
+// CIIRFilter / RIIRFilter(Bc, Ac) (iirfilter.hpp:23-59, 133-169): transfer function form
+struct TFIIR : IIR {
+    TFIIR(const py::handle& bc, const py::handle& ac, bool c)
+    {
+        cplx = c;
+        std::vector<float> b = to_fvec(bc), a = to_fvec(ac);
+        check(ldsp_iirfilt_create_tf(b.data(), (unsigned)b.size(), a.data(), (unsigned)a.size(), c ? 1 : 0, &q));
+    }
+};
+
+// C/R{Lowpass,Highpass,Bandpass,Bandstop}IIR (iirfilter.hpp:61-131, 171-241)
+struct BandIIR : IIR {
+    BandIIR(const std::string& typ, int order, float fc, float f0, float ap, float as, int btype, bool c)
+    {
+        cplx = c;
+        if (order < 1) throw py::value_error("iirfilt: order must be >= 1");
+        check(ldsp_iirfilt_create_prototype(ftype_of(typ), btype, (unsigned)order, fc, f0, ap, as, c ? 1 : 0, &q));
+    }
+};
+
+// ComplexIIRFilter / RealIIRFilter (iirfilter.hpp:243-356)
+struct ProtoIIR : IIR {
+    std::string mFt, mBt;
+    int mOrder;
+    float mFc, mF0, mAp, mAs;
+    ProtoIIR(const std::string& ft, const std::string& bt, int order, float fc, float f0, float ap, float as, bool c)
+        : mOrder(order), mFc(fc), mF0(f0), mAp(ap), mAs(as)
+    {
+        cplx = c;
+        int fti = 0, bti = 0;
+        auto fi = kFilterTypes.find(ft);
+        if (fi != kFilterTypes.end()) {
+            mFt = ft;
+            fti = fi->second;
+        }
+        auto bi = kBandTypes.find(bt);
+        if (bi != kBandTypes.end()) {
+            mBt = bt;
+            bti = bi->second;
+        }
+        if (order < 1) throw py::value_error("iirfilt: order must be >= 1");
+        check(ldsp_iirfilt_create_prototype(fti, bti, (unsigned)order, fc, f0, ap, as, c ? 1 : 0, &q));
+    }
+};
+
+// DeemphasisFilter (iirfilter.hpp:358-392): 75 us one-pole, b = [1-x], a = [1, -x]
+struct DeemphasisFilter : IIR {
+    explicit DeemphasisFilter(float sr)
+    {
+        cplx = false;
+        const float x = (float)exp(-1.0 / (75.0E-6 * (double)sr));
+        float mA[2], mB[1];
+        mA[0] = 1.0f;
+        mA[1] = -x;
+        mB[0] = (float)(1.0 - (double)x);
+        check(ldsp_iirfilt_create_tf(mB, 1, mA, 2, 0, &q));
+    }
+};
+
+// ------------------------------------------------------------------ NCO (nco.hpp:4-81)
+struct NCO {
+    ldsp_nco_t q = nullptr;
+    std::string mType;
+    explicit NCO(const std::string& type)
+    {
+        mType = (type == "nco") ? "nco" : "vco";
+        check(ldsp_nco_create(type == "nco" ? 0 : 1, &q));
+    }
+    NCO(const NCO&) = delete;
+    ~NCO() { if (q) ldsp_nco_destroy(q); }
+    float frequency()
+    {
+        float f;
+        check(ldsp_nco_get_frequency(q, &f));
+        return f;
+    }
+    void set_frequency(float f) { check(ldsp_nco_set_frequency(q, f)); }
+    void adjust_frequency(float df) { check(ldsp_nco_adjust_frequency(q, df)); }
+    float phase()
+    {
+        float p;
+        check(ldsp_nco_get_phase(q, &p));
+        return p;
+    }
+    void set_phase(float p) { check(ldsp_nco_set_phase(q, p)); }
+    void adjust_phase(float dp) { check(ldsp_nco_adjust_phase(q, dp)); }
+    void set_pll_bandwidth(float bw) { check(ldsp_nco_pll_set_bandwidth(q, bw)); }
+    void pll_step(float dph) { check(ldsp_nco_pll_step(q, dph)); }
+    void print()
+    {
+        py::print(py::str("<liquid.nco_crcf, type={}, phase={:.6f}, freq={:.6f}>").format(mType, phase(), frequency()));
+    }
+    py::tuple state()
+    {
+        uint32_t t, d;
+        check(ldsp_nco_get_state(q, &t, &d));
+        return py::make_tuple(t, d);
+    }
+    py::object mix(const py::handle& x, bool down)
+    {
+        return run_same(x, true, true, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            return ldsp_nco_mix(q, xi, n, yo, down ? 1 : 0, mem, s);
+        });
+    }
+};
+
+// ------------------------------------------------------------------ AGC (agc.hpp:4-149)
+// AGC::execute keeps `static int state_last` shared by every instance (agc.hpp:110)
+int g_state_last = 0;   // LIQUID_AGC_SQUELCH_UNKNOWN
+
+struct AGC {
+    ldsp_agc_t q = nullptr;
+    bool mSquelch = false, mLock = false;
+    py::object mOnRise = py::none();
+    AGC() { check(ldsp_agc_create(&q)); }
+    AGC(const AGC&) = delete;
+    ~AGC() { if (q) ldsp_agc_destroy(q); }
+    template <typename T, typename G>
+    T get(G g)
+    {
+        T v;
+        check(g(q, &v));
+        return v;
+    }
+    void set_bandwidth(float bw) { check(ldsp_agc_set_bandwidth(q, bw)); }
+    float get_bandwidth() { return get<float>(ldsp_agc_get_bandwidth); }
+    bool get_squelch() { return mSquelch; }
+    void set_squelch(bool v)
+    {
+        mSquelch = v;
+        check(ldsp_agc_squelch_enable(q, v ? 1 : 0));
+    }
+    void set_threshold(double t) { check(ldsp_agc_squelch_set_threshold(q, (float)t)); }
+    double get_threshold() { return get<float>(ldsp_agc_squelch_get_threshold); }
+    float get_level() { return get<float>(ldsp_agc_get_signal_level); }
+    void set_level(float l) { check(ldsp_agc_set_signal_level(q, l)); }
+    float get_rssi() { return get<float>(ldsp_agc_get_rssi); }
+    void set_rssi(float r) { check(ldsp_agc_set_rssi(q, r)); }
+    bool get_lock() { return mLock; }
+    void set_lock(bool v)
+    {
+        mLock = v;
+        check(ldsp_agc_lock(q, v ? 1 : 0));
+    }
+    float get_gain() { return get<float>(ldsp_agc_get_gain); }
+    void set_gain(float g) { check(ldsp_agc_set_gain(q, g)); }
+    float get_scale() { return get<float>(ldsp_agc_get_scale); }
+    void set_scale(float s) { check(ldsp_agc_set_scale(q, s)); }
+    int status() { return get<int>(ldsp_agc_squelch_get_status); }
+    void reset() { check(ldsp_agc_reset(q)); }
+    void print()
+    {
+        py::print(py::str("<liquid.agc_crcf, rssi={:.4f} dB, gain={:.6f}, bw={:.4f}, locked={}, squelch={}>")
+                      .format(get_rssi(), get_gain(), get_bandwidth(), mLock ? "yes" : "no",
+                              mSquelch ? "enabled" : "disabled"));
+    }
+    py::object call(const py::handle& x)
+    {
+        // Per-sample squelch statuses are needed only while squelch is enabled
+        // (otherwise every status is LIQUID_AGC_SQUELCH_DISABLED).
+        std::vector<uint8_t> st;
+        const bool need = mSquelch;
+        py::object out = run_same(x, true, true, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            if (need) st.resize(n);
+            return ldsp_agc_execute(q, xi, n, yo, need ? st.data() : nullptr, mem, s);
+        });
+        const size_t n = py::len(out);
+        if (!need) {
+            if (n > 0) g_state_last = 7;
+            return out;
+        }
+        // replay the onRise transitions in order (after the block; documented)
+        for (size_t i = 0; i < st.size(); i++) {
+            const int state = st[i];
+            if (state != g_state_last) {
+                g_state_last = state;
+                if (state == 2 && !mOnRise.is_none()) mOnRise();
+            }
+        }
+        return out;
+    }
+};
+
+// ------------------------------------------------------------------ AmpModem (demod.hpp:221-307)
+const std::map<std::string, int> kAmpTypes = {{"dsb", 0}, {"usb", 1}, {"lsb", 2}};
+
+struct AmpModem {
+    float mModulation;
+    std::string mType;
+    bool mCarrier;
+    ldsp_ampmodem_t q = nullptr;
+    AmpModem(float mod, const std::string& type, bool car) : mModulation(mod), mCarrier(car) { make(mod, type, car); }
+    AmpModem(const AmpModem&) = delete;
+    ~AmpModem() { destroy(); }
+    void destroy()
+    {
+        if (q) ldsp_ampmodem_destroy(q);
+        q = nullptr;
+    }
+    void make(float mod, const std::string& type, bool car)
+    {
+        int mt = 0;
+        auto it = kAmpTypes.find(type);
+        if (it != kAmpTypes.end()) {
+            mType = type;
+            mt = it->second;
+        }
+        check(ldsp_ampmodem_create(mod, mt, car ? 0 : 1, &q));
+    }
+    void set_type(const std::string& type)
+    {
+        if (type == "dsb" || type == "usb" || type == "lsb") {
+            mType = type;
+            destroy();
+            make(mModulation, mType, mCarrier);
+        }
+    }
+    std::string get_type() { return mType; }
+    void set_modulation(float m)
+    {
+        mModulation = m;
+        destroy();
+        make(mModulation, mType, mCarrier);
+    }
+    float get_modulation() { return mModulation; }
+    void set_carrier(bool c)
+    {
+        mCarrier = c;
+        destroy();
+        make(mModulation, mType, mCarrier);
+    }
+    bool get_carrier() { return mCarrier; }
+    void reset() { check(ldsp_ampmodem_reset(q)); }
+    void print()
+    {
+        py::print(py::str("<liquid.ampmodem, type=\"{}\", carrier_suppressed={}, mod_index={:.6f}>")
+                      .format(mType.empty() ? "dsb" : mType, mCarrier ? "false" : "true", mModulation));
+    }
+    py::tuple pll_state()
+    {
+        uint32_t t, d;
+        check(ldsp_ampmodem_get_pll_state(q, &t, &d));
+        return py::make_tuple(t, d);
+    }
+    py::object demod(const py::handle& x)
+    {
+        return run_same(x, true, false, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            return ldsp_ampmodem_demodulate(q, xi, n, yo, mem, s);
+        });
+    }
+};
+
+
+// distinct C++ types for the distinct Python classes
+struct RealResampler : Resampler {
+    RealResampler(float r, int d, float fc, float as, int nf) : Resampler(r, d, fc, as, nf, false) {}
+};
+struct ComplexResampler : Resampler {
+    ComplexResampler(float r, int d, float fc, float as, int nf) : Resampler(r, d, fc, as, nf, true) {}
+};
+struct CIIRFilter : TFIIR {
+    CIIRFilter(const py::handle& b, const py::handle& a) : TFIIR(b, a, true) {}
+};
+struct RIIRFilter : TFIIR {
+    RIIRFilter(const py::handle& b, const py::handle& a) : TFIIR(b, a, false) {}
+};
+template <int BT, bool CPLX>
+struct PassIIR : BandIIR {
+    // Lowpass / Highpass hard-code f0 = 0.1 (iirfilter.hpp:70,88,180,198)
+    PassIIR(const std::string& t, int order, float fc, float ap, float as) : BandIIR(t, order, fc, 0.1f, ap, as, BT, CPLX) {}
+};
+template <int BT, bool CPLX>
+struct BandXIIR : BandIIR {
+    BandXIIR(const std::string& t, int order, float fc, float f0, float ap, float as)
+        : BandIIR(t, order, fc, f0, ap, as, BT, CPLX) {}
+};
+struct ComplexIIRFilter : ProtoIIR {
+    ComplexIIRFilter(const std::string& ft, const std::string& bt, int o, float fc, float f0, float ap, float as)
+        : ProtoIIR(ft, bt, o, fc, f0, ap, as, true) {}
+};
+struct RealIIRFilter : ProtoIIR {
+    RealIIRFilter(const std::string& ft, const std::string& bt, int o, float fc, float f0, float ap, float as)
+        : ProtoIIR(ft, bt, o, fc, f0, ap, as, false) {}
+};
+
+template <typename C, typename P>
+void bind_iir_common(P& c)
+{
+    c.def("reset", &C::reset)
+        .def("freqresponse", &C::freqresponse)
+        .def("__call__", &C::call)
+        .def_property("exact", &C::get_exact, &C::set_exact)
+        .def("sos", &C::sos);
+}
+
+template <typename C>
+void bind_pass(py::module_& m, const char* name)
+{
+    py::class_<C> c(m, name);
+    c.def(py::init<std::string, int, float, float, float>(), py::arg("filter_type") = "butter", py::arg("order"),
+          py::arg("Fc"), py::arg("Ap") = 0.5f, py::arg("As") = 20.0f);
+    bind_iir_common<C>(c);
+}
+template <typename C>
+void bind_band(py::module_& m, const char* name)
+{
+    py::class_<C> c(m, name);
+    c.def(py::init<std::string, int, float, float, float, float>(), py::arg("filter_type") = "butter",
+          py::arg("order"), py::arg("Fc"), py::arg("F0"), py::arg("Ap") = 0.5f, py::arg("As") = 20.0f);
+    bind_iir_common<C>(c);
+}
+template <typename C>
+void bind_proto(py::module_& m, const char* name)
+{
+    py::class_<C> c(m, name);
+    c.def(py::init<std::string, std::string, int, float, float, float, float>(), py::arg("filter_type") = "butter",
+          py::arg("band_type") = "lowpass", py::arg("order") = 2, py::arg("Fc") = 0.2f, py::arg("F0") = 0.3f,
+          py::arg("Ap") = 0.7f, py::arg("As") = 60.0)
+        .def_readonly("filter_type", &C::mFt)
+        .def_readonly("band_type", &C::mBt)
+        .def_readonly("order", &C::mOrder)
+        .def_readonly("Fc", &C::mFc)
+        .def_readonly("F0", &C::mF0)
+        .def_readonly("Ap", &C::mAp)
+        .def_readonly("As", &C::mAs)
+        .def("freqresponse", &C::freqresponse)
+        .def("__call__", &C::call)
+        .def("print", &C::print)
+        .def("reset", &C::reset)
+        .def_property("exact", &C::get_exact, &C::set_exact)
+        .def("sos", &C::sos);
+}
+
+const char* kResampDoc = "Arbitrary-rate polyphase resampler (liquid resamp_*), runs on the GPU.";
+const char* kResampInitDoc =
+    "rate: output/input rate; len: filter semi-length m (20); Fc: anti-alias cutoff; As: stop-band "
+    "attenuation in dB (60); nfilter: polyphase branches (13, rounded up to a power of two)";
+const char* kAgcDoc = "Automatic gain control with squelch for complex IQ (liquid agc_crcf), runs on the GPU.";
+
+} // namespace
+
+PYBIND11_MODULE(_liquiddsp, m)
+{
+    m.doc() = "MI355X-native replacement for python-liquiddsp's streaming DSP classes (libldsp C ABI)";
+    m.attr("__backend__") = "libldsp (HIP, gfx950)";
+
+    m.def("device_count", [] {
+        int n = 0;
+        check(ldsp_device_count(&n));
+        return n;
+    });
+    m.def("_math_eval", [](int fn, uintptr_t a, uintptr_t b, uintptr_t y, size_t n, uintptr_t stream) {
+        check(ldsp_debug_math_eval(fn, (const float*)a, (const float*)b, (float*)y, n, (void*)stream));
+    });
+
+    // ---- CIIRFilter / RIIRFilter (wrapper.cpp:30-34, 82-86)
+    {
+        py::class_<CIIRFilter> c(m, "CIIRFilter");
+        c.def(py::init<py::handle, py::handle>(), py::arg("Bc"), py::arg("Ac"));
+        bind_iir_common<CIIRFilter>(c);
+    }
+    {
+        py::class_<RIIRFilter> c(m, "RIIRFilter");
+        c.def(py::init<py::handle, py::handle>(), py::arg("Bc"), py::arg("Ac"));
+        bind_iir_common<RIIRFilter>(c);
+    }
+    // ---- pass / band families (wrapper.cpp:36-132)
+    bind_pass<PassIIR<0, true>>(m, "CLowpassIIR");
+    bind_pass<PassIIR<1, true>>(m, "CHighpassIIR");
+    bind_band<BandXIIR<2, true>>(m, "CBandpassIIR");
+    bind_band<BandXIIR<3, true>>(m, "CBandstopIIR");
+    bind_pass<PassIIR<0, false>>(m, "RLowpassIIR");
+    bind_pass<PassIIR<1, false>>(m, "RHighpassIIR");
+    bind_band<BandXIIR<2, false>>(m, "RBandpassIIR");
+    bind_band<BandXIIR<3, false>>(m, "RBandstopIIR");
+    // ---- ComplexIIRFilter / RealIIRFilter (wrapper.cpp:134-172)
+    bind_proto<ComplexIIRFilter>(m, "ComplexIIRFilter");
+    bind_proto<RealIIRFilter>(m, "RealIIRFilter");
+
+    // ---- DeemphasisFilter (wrapper.cpp:178-181)
+    py::class_<DeemphasisFilter>(m, "DeemphasisFilter")
+        .def(py::init<float>(), py::arg("sample_rate") = 48000)
+        .def("freqresponse", &DeemphasisFilter::freqresponse)
+        .def("__call__", &DeemphasisFilter::call)
+        .def("reset", &DeemphasisFilter::reset);
+
+    // ---- AmpModem (wrapper.cpp:189-199)
+    py::class_<AmpModem>(m, "AmpModem")
+        .def(py::init<float, std::string, bool>(), py::arg("modulation") = 0.75, py::arg("type") = "dsb",
+             py::arg("carrier") = false)
+        .def_property("modulation", &AmpModem::get_modulation, &AmpModem::set_modulation)
+        .def_property("type", &AmpModem::get_type, &AmpModem::set_type)
+        .def_property("carrier", &AmpModem::get_carrier, &AmpModem::set_carrier)
+        .def("print", &AmpModem::print)
+        .def("reset", &AmpModem::reset)
+        .def("pll_state", &AmpModem::pll_state)
+        .def("__call__", &AmpModem::demod);
+
+    // ---- NCO (wrapper.cpp:201-212)
+    py::class_<NCO>(m, "NCO")
+        .def(py::init<std::string>(), py::arg("type") = "nco")
+        .def("print", &NCO::print)
+        .def_property("freq", &NCO::frequency, &NCO::set_frequency)
+        .def("adjust_frequency", &NCO::adjust_frequency)
+        .def("adjust_phase", &NCO::adjust_phase)
+        .def_property("phase", &NCO::phase, &NCO::set_phase)
+        .def("set_pll_bandwidth", &NCO::set_pll_bandwidth)
+        .def("pll_step", &NCO::pll_step)
+        .def("state", &NCO::state)
+        .def("__call__", [](NCO& n, const py::handle& x) { return n.mix(x, false); })
+        .def("mix_up", [](NCO& n, const py::handle& x) { return n.mix(x, false); })
+        .def("mix_down", [](NCO& n, const py::handle& x) { return n.mix(x, true); });
+
+    // ---- RealResampler / ComplexResampler (wrapper.cpp:214-226)
+    py::class_<RealResampler>(m, "RealResampler", kResampDoc)
+        .def(py::init<float, int, float, float, int>(), py::arg("rate"), py::arg("len") = 20, py::arg("Fc"),
+             py::arg("As") = 60.0f, py::arg("nfilter") = 13, kResampInitDoc)
+        .def("print", &RealResampler::print)
+        .def("reset", &RealResampler::reset)
+        .def("__call__", &RealResampler::call)
+        .def_property("rate", &RealResampler::get_rate, &RealResampler::set_rate);
+    py::class_<ComplexResampler>(m, "ComplexResampler", kResampDoc)
+        .def(py::init<float, int, float, float, int>(), py::arg("rate"), py::arg("len") = 20, py::arg("Fc"),
+             py::arg("As") = 60.0f, py::arg("nfilter") = 13, kResampInitDoc)
+        .def("print", &ComplexResampler::print)
+        .def("reset", &ComplexResampler::reset)
+        .def("__call__", &ComplexResampler::call)
+        .def_property("rate", &ComplexResampler::get_rate, &ComplexResampler::set_rate);
+
+    // ---- AGC (wrapper.cpp:228-242)
+    py::class_<AGC>(m, "AGC", kAgcDoc)
+        .def(py::init<>())
+        .def_property("squelch", &AGC::get_squelch, &AGC::set_squelch)
+        .def_property("threshold", &AGC::get_threshold, &AGC::set_threshold)
+        .def_property("bandwidth", &AGC::get_bandwidth, &AGC::set_bandwidth)
+        .def_property("level", &AGC::get_level, &AGC::set_level)
+        .def_property("level_dB", &AGC::get_rssi, &AGC::set_rssi)
+        .def_property("lock", &AGC::get_lock, &AGC::set_lock)
+        .def_property("gain", &AGC::get_gain, &AGC::set_gain)
+        .def_property("scale", &AGC::get_scale, &AGC::set_scale)
+        .def_property_readonly("status", &AGC::status)
+        .def_property(
+            "onRise", [](AGC& a) { return a.mOnRise; }, [](AGC& a, py::object f) { a.mOnRise = f; })
+        .def("print", &AGC::print)
+        .def("reset", &AGC::reset)
+        .def("__call__", &AGC::call);
+
+    // ---- FIR family (wrapper.cpp:244-257) + the new ComplexFIRFilter
+    py::class_<RealFIRFilter>(m, "RealFIRFilter")
+        .def(py::init<py::handle>(), py::arg("h"))
+        .def("freqresponse", &RealFIRFilter::freqresponse)
+        .def("__call__", &RealFIRFilter::call)
+        .def("reset", &RealFIRFilter::reset)
+        .def_property("exact", &RealFIRFilter::get_exact, &RealFIRFilter::set_exact)
+        .def_property_readonly("taps", &RealFIRFilter::taps);
+    py::class_<ComplexFIRFilter>(m, "ComplexFIRFilter")
+        .def(py::init<py::handle>(), py::arg("h"))
+        .def("freqresponse", &ComplexFIRFilter::freqresponse)
+        .def("__call__", &ComplexFIRFilter::call)
+        .def("reset", &ComplexFIRFilter::reset)
+        .def_property("exact", &ComplexFIRFilter::get_exact, &ComplexFIRFilter::set_exact)
+        .def_property_readonly("taps", &ComplexFIRFilter::taps);
+    py::class_<RealDCBlocker>(m, "RealDCBlocker")
+        .def(py::init<int, float>(), py::arg("slen") = 25, py::arg("As") = 20.0f)
+        .def("freqresponse", &RealDCBlocker::freqresponse)
+        .def("__call__", &RealDCBlocker::call)
+        .def("reset", &RealDCBlocker::reset)
+        .def_property("exact", &RealDCBlocker::get_exact, &RealDCBlocker::set_exact)
+        .def_property_readonly("taps", &RealDCBlocker::taps);
+    py::class_<RealKaiserBessel>(m, "RealKaiserBessel")
+        .def(py::init<int, float, float, float>(), py::arg("flen") = 25, py::arg("Fc"), py::arg("As") = 20.0f,
+             py::arg("offset") = 0.0f)
+        .def("freqresponse", &RealKaiserBessel::freqresponse)
+        .def("__call__", &RealKaiserBessel::call)
+        .def("reset", &RealKaiserBessel::reset)
+        .def_property("exact", &RealKaiserBessel::get_exact, &RealKaiserBessel::set_exact)
+        .def_property_readonly("taps", &RealKaiserBessel::taps)
+        .def_property_readonly("scale", &RealKaiserBessel::get_scale);
+}
