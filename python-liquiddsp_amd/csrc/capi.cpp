@@ -6,6 +6,8 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -1204,11 +1206,11 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         uint8_t* dstat = status ? (uint8_t*)q->status.ensure(std::max<size_t>(n, 1), q->device) : nullptr;
         if (n > 0) {
             const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
-            const int W = (int)std::min(1 << 20, std::max(2048, (int)(64.0f / a)));
+            const int W = (int)std::min(1 << 20, std::max(2048, (int)(80.0f / a)));
             if (n >= (size_t)4 * W) {
                 k::SpecPlan p;
                 p.W = W;
-                p.C = 512;
+                p.C = 256;
                 p.nchunks = (long)((n + p.C - 1) / p.C);
                 p.scratch = q->scratch.ensure((size_t)p.nchunks * 8 * sizeof(unsigned), q->device);
                 k::agc_spec(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
@@ -1303,6 +1305,14 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
             void* pscr = q->pll.ensure(k::pll_scratch_bytes(n), q->device);
             k::ampmodem_pll(x0, dx, q->dlh[q->cur].p, q->dlh[1 - q->cur].p, (int)q->m, n, q->dst.as<k::AmpState>(),
                             q->dtab.as<float>(), q->mod_index, q->suppressed ? 1 : 0, mbuf, pscr, e.stream);
+            if (n >= 8192 && std::getenv("LDSP_DEBUG_PLL")) {
+                unsigned long long stt[4];
+                LDSP_HIP(hipMemcpyAsync(stt, (char*)pscr + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
+                                        e.stream));
+                LDSP_HIP(hipStreamSynchronize(e.stream));
+                std::fprintf(stderr, "[ldsp pll] n=%zu repairs=%llu unused=%llu walk_clk=%llu wait_clk=%llu\n", n, stt[0],
+                             stt[1], stt[2], stt[3]);
+            }
             if (!q->suppressed)
                 k::fir_exact(false, mbuf, q->dch[q->cur].p, q->dch[1 - q->cur].p, n, q->ddc.as<float>(), L, 1.0f,
                              dy, e.stream);

@@ -14,18 +14,20 @@
 // sample.  Exact trajectories never coalesce (the quantised phase detector
 // keeps a residual), so chunk-parallel speculation cannot be verified by state
 // equality as for the AGC; instead:
-//   k_pll_cand : every chunk of C samples runs W samples early from an
+//   k_pll_cand : every chunk of 256 samples runs W samples early from an
 //                extrapolated state and records, per sample, its phase and the
 //                kick / output differences of the neighbouring indices i-1, i+1;
-//   k_pll_walk : one workgroup walks the chunks in order with the exact offset
+//   k_pll_walk : one workgroup walks 1024-sample blocks in order with the exact offset
 //                of the true trajectory from the candidate; a 64-lane ballot
 //                finds the next sample whose true index differs, only that
 //                sample is recomputed (a table lookup of the recorded neighbour
 //                for |di| = 1, the full loop step otherwise), the offset is
-//                updated, and the output is patched.  Waves 1-3 stream the next
-//                chunk's records into an LDS double buffer meanwhile.
+//                updated, and the output is patched.  Waves 1-7 stream the next
+//                block's records into an LDS double buffer meanwhile.
 // The result is bit-identical to the sequential loop (k_pll_seq, also used for
 // short calls); ~2 % of samples need a repair on locked AM signals.
+#include <cstdlib>
+
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 #include "ldsp_math.hpp"
@@ -35,7 +37,9 @@ namespace k {
 
 namespace {
 
-constexpr int kChunk = 1024;      // candidate chunk = walker block
+constexpr int kBlk = 1024;        // walker block
+constexpr int kCand = 256;        // candidate chunk
+constexpr int kSub = kBlk / kCand;
 constexpr int kWarm = 2048;       // candidate warm-up
 
 __device__ __forceinline__ uint32_t tidx(uint32_t th) { return ((th + (1u << 21)) >> 22) & 0x3ffu; }
@@ -112,25 +116,86 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
 }
 
 // ------------------------------------------------------------------ candidates
-// records (SoA, stride npad): th, dk1m, dk2m, dk1p, dk2p (uint32), om, op (float)
+// Candidate chunks are kCand samples; the walker consumes blocks of kBlk =
+// kSub candidate chunks.  Records (AoS, 8 words = 32 B per sample, npad = nblk*kBlk):
+//   th (candidate phase), u = (th + 2^21) mod 2^22 (position inside the table
+//   cell), dk1(i-1), dk2(i-1), dk1(i+1), dk2(i+1) (kick differences to index
+//   i), output at i-1, i+1 (float bits).
 struct CandBuf {
-    uint32_t* th;
-    uint32_t* dk;         // [4][npad]: dk1(i-1), dk2(i-1), dk1(i+1), dk2(i+1)   (difference to index i)
-    float* om;            // [2][npad]: output at i-1, i+1
-    uint32_t* cs;         // [nch][2] candidate state at chunk start
-    uint32_t* ce;         // [nch][2] candidate state at chunk end
+    uint4* rec;           // [npad][2]
+    uint32_t* cs;         // [nsub][2] candidate state at chunk start
+    uint32_t* ce;         // [nsub][2] candidate state at chunk end
+    unsigned long long* stats;   // walker counters: repairs, -, walk ticks, barrier-wait ticks
     long npad;
+    int dbg;              // timing experiments only (LDSP_DEBUG_PLL_MODE): 1 = skip repairs
 };
 
-__global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpState* st, long nch, CandBuf cb,
+__device__ __forceinline__ const float2* x1_ptr(const PllIn& in, long i)
+{
+    const long g = i - in.m;
+    return g >= 0 ? in.x + g : in.hist + (g + in.m);
+}
+
+// Run the loop over [a, b) with the inputs software-pipelined kB samples ahead
+// (the loads are off the theta dependence chain).  REC: record the candidate.
+constexpr int kB = 8;
+template <bool REC>
+__device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long a, long b, float alpha, float beta,
+                                         uint32_t& theta, uint32_t& d, const CandBuf& cb, float* __restrict__ y)
+{
+    if (a >= b) return;
+    float2 n0[kB], n1[kB];
+#pragma unroll
+    for (int j = 0; j < kB; j++) {
+        const long i = min(a + j, b - 1);
+        n0[j] = in.x0[i];
+        n1[j] = *x1_ptr(in, i);
+    }
+    for (long i = a; i < b; i += kB) {
+        float2 c0[kB], c1[kB];
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            c0[j] = n0[j];
+            c1[j] = n1[j];
+        }
+        if (i + kB < b) {
+#pragma unroll
+            for (int j = 0; j < kB; j++) {
+                const long ii = min(i + kB + j, b - 1);
+                n0[j] = in.x0[ii];
+                n1[j] = *x1_ptr(in, ii);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            if (i + j < b) {
+                const uint32_t ic = tidx(theta);
+                const Kick kc = pll_eval(tab, ic, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
+                if (REC) {
+                    const long s = i + j;
+                    const Kick km = pll_eval(tab, (ic - 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
+                    const Kick kp = pll_eval(tab, (ic + 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
+                    cb.rec[2 * s] = make_uint4(theta, (theta + (1u << 21)) & 0x3fffffu, km.k1 - kc.k1, km.k2 - kc.k2);
+                    cb.rec[2 * s + 1] = make_uint4(kp.k1 - kc.k1, kp.k2 - kc.k2, __float_as_uint(km.out),
+                                                   __float_as_uint(kp.out));
+                    y[s] = kc.out;
+                }
+                d += kc.k1;
+                theta += kc.k2 + d;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpState* st, long nchc, CandBuf cb,
                                                  float* __restrict__ y)
 {
     __shared__ float tab[1024];
     for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = in.table[i];
     __syncthreads();
     const long k = (long)blockIdx.x * 64 + threadIdx.x;
-    if (k >= nch) return;
-    const long s0 = k * kChunk, s1 = min(n, s0 + kChunk);
+    if (k >= nchc) return;
+    const long s0 = k * kCand, s1 = min(n, s0 + kCand);
     const float alpha = st->alpha, beta = st->beta;
     uint32_t theta = st->theta, d = st->dtheta;
     long w0 = s0 - kWarm;
@@ -139,136 +204,239 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpStat
     } else {
         theta = st->theta + (uint32_t)((uint64_t)w0 * d);   // constant-frequency extrapolation
     }
-    for (long i = w0; i < s0; i++) {
-        const Kick kk = pll_eval(tab, tidx(theta), in.x0[i], x1_at(in, i), alpha, beta, in.mod_index, in.costas);
-        d += kk.k1;
-        theta += kk.k2 + d;
-    }
+    cand_run<false>(in, tab, w0, s0, alpha, beta, theta, d, cb, y);
     cb.cs[2 * k] = theta;
     cb.cs[2 * k + 1] = d;
-    for (long i = s0; i < s1; i++) {
-        const float2 u0 = in.x0[i], u1 = x1_at(in, i);
-        const uint32_t ic = tidx(theta);
-        const Kick kc = pll_eval(tab, ic, u0, u1, alpha, beta, in.mod_index, in.costas);
-        const Kick km = pll_eval(tab, (ic - 1) & 0x3ffu, u0, u1, alpha, beta, in.mod_index, in.costas);
-        const Kick kp = pll_eval(tab, (ic + 1) & 0x3ffu, u0, u1, alpha, beta, in.mod_index, in.costas);
-        cb.th[i] = theta;
-        cb.dk[i] = km.k1 - kc.k1;
-        cb.dk[cb.npad + i] = km.k2 - kc.k2;
-        cb.dk[2 * cb.npad + i] = kp.k1 - kc.k1;
-        cb.dk[3 * cb.npad + i] = kp.k2 - kc.k2;
-        cb.om[i] = km.out;
-        cb.om[cb.npad + i] = kp.out;
-        y[i] = kc.out;
-        d += kc.k1;
-        theta += kc.k2 + d;
-    }
+    cand_run<true>(in, tab, s0, s1, alpha, beta, theta, d, cb, y);
     cb.ce[2 * k] = theta;
     cb.ce[2 * k + 1] = d;
 }
 
 // ------------------------------------------------------------------ walker
 struct WalkBuf {
-    uint32_t th[kChunk];
-    uint32_t dk[4][kChunk];
-    float om[2][kChunk];
-    uint32_t cs[2], ce[2];
+    uint4 rec[kBlk * 2];
+    uint32_t cs[kSub * 2], ce[kSub * 2];
 };
 
-__device__ __forceinline__ void walk_load(WalkBuf& b, const CandBuf& cb, long chunk, long n, int t, int nt)
+constexpr int kWalkThreads = 512;
+constexpr int kLoaders = kWalkThreads - 64;       // waves 1..7
+constexpr int kVec = kBlk * 2;                    // uint4 per block
+constexpr int kLoadSlots = (kVec + kLoaders - 1) / kLoaders;
+
+struct LoadRegs {
+    uint4 v[kLoadSlots];
+    uint32_t w;
+};
+
+__device__ __forceinline__ void walk_fetch(LoadRegs& r, const CandBuf& cb, long blk, int lt)
 {
-    const long s0 = chunk * kChunk;
-    const int cnt = (int)min((long)kChunk, n - s0);
-    for (int i = t; i < cnt; i += nt) {
-        b.th[i] = cb.th[s0 + i];
-        b.dk[0][i] = cb.dk[s0 + i];
-        b.dk[1][i] = cb.dk[cb.npad + s0 + i];
-        b.dk[2][i] = cb.dk[2 * cb.npad + s0 + i];
-        b.dk[3][i] = cb.dk[3 * cb.npad + s0 + i];
-        b.om[0][i] = cb.om[s0 + i];
-        b.om[1][i] = cb.om[cb.npad + s0 + i];
+    const uint4* src = cb.rec + blk * kVec;
+#pragma unroll
+    for (int k = 0; k < kLoadSlots; k++) {
+        const int q = lt + k * kLoaders;
+        if (q < kVec) r.v[k] = src[q];
     }
-    if (t == 0) {
-        b.cs[0] = cb.cs[2 * chunk];
-        b.cs[1] = cb.cs[2 * chunk + 1];
-        b.ce[0] = cb.ce[2 * chunk];
-        b.ce[1] = cb.ce[2 * chunk + 1];
+    r.w = lt < 2 * kSub ? cb.cs[blk * 2 * kSub + lt]
+                        : (lt < 4 * kSub ? cb.ce[blk * 2 * kSub + lt - 2 * kSub] : 0u);
+}
+
+__device__ __forceinline__ void walk_store(WalkBuf& b, const LoadRegs& r, int lt)
+{
+#pragma unroll
+    for (int k = 0; k < kLoadSlots; k++) {
+        const int q = lt + k * kLoaders;
+        if (q < kVec) b.rec[q] = r.v[k];
+    }
+    if (lt < 2 * kSub) b.cs[lt] = r.w;
+    else if (lt < 4 * kSub) b.ce[lt - 2 * kSub] = r.w;
+}
+
+// Inputs of the rare full step (true index more than one cell from the candidate's).
+struct FullCtx {
+    const float2* x0;
+    const float2* x;
+    const float2* hist;
+    const float* table;
+    int m, costas;
+    float alpha, beta, mod_index;
+};
+
+// Kick differences and output of the true index (icand + t) at global sample sg.
+__device__ __noinline__ uint4 pll_full(FullCtx fc, uint32_t thc, uint32_t t, long sg)
+{
+    const uint32_t ic = tidx(thc);
+    const uint32_t it = (ic + t) & 0x3ffu;
+    const long g = sg - fc.m;
+    const float2 u0 = fc.x0[sg], u1 = g >= 0 ? fc.x[g] : fc.hist[g + fc.m];
+    const Kick kt = pll_eval(fc.table, it, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas);
+    const Kick kc = pll_eval(fc.table, ic, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas);
+    return make_uint4(kt.k1 - kc.k1, kt.k2 - kc.k2, __float_as_uint(kt.out), 0u);
+}
+
+__device__ __forceinline__ void load_sub(uint4 (&D)[4][2], const WalkBuf& b, int sub, int lane)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int i = sub * kCand + q * 64 + lane;
+        D[q][0] = b.rec[2 * i];
+        D[q][1] = b.rec[2 * i + 1];
     }
 }
 
-__global__ void __launch_bounds__(256) k_pll_walk(PllIn in, long n, AmpState* st, long nch, CandBuf cb,
-                                                  float* __restrict__ y)
+__device__ __forceinline__ uint32_t rl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
+
+// Walk one candidate chunk (4 lane-blocks of 64 samples) from local sample
+// base0.  On entry dtheta(base0 + l) = K + l*DD (ldd = lane*DD); on exit K is
+// the offset at the chunk end (or at cnt for the last, partial chunk).
+template <bool FULL>
+__device__ __forceinline__ void walk_sub(const uint4 (&D)[4][2], int base0, int cnt, uint32_t& K, uint32_t& DD,
+                                         uint32_t& ldd, float* __restrict__ yb, long sb, int lane, const FullCtx& fc,
+                                         unsigned long long& n_rep, int dbg)
 {
-    __shared__ float tab[1024];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int base = base0 + q * 64;
+        int nvalid = 64;
+        if (!FULL) {
+            nvalid = min(64, cnt - base);
+            if (nvalid <= 0) return;
+        }
+        const uint32_t u = D[q][0].y;
+        unsigned long long M = (FULL || nvalid == 64) ? ~0ull : ((1ull << nvalid) - 1ull);
+        unsigned long long PM = 0;
+        uint32_t pout = 0;
+        if (dbg != 1) while (true) {
+            // index of th + off equals index of th  <=>  u + off < 2^22 (mod 2^32)
+            const uint32_t v = u + K + ldd;
+            const unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
+            if (mask == 0) break;
+            const int j = __builtin_ctzll(mask);
+            // side of the mismatch from two more ballots (SALU bit tests, no readlane of v)
+            const unsigned long long upm = __builtin_amdgcn_ballot_w64(v - 0x400000u < 0x400000u);   // di = +1
+            const unsigned long long dnm = __builtin_amdgcn_ballot_w64(v >= 0xffc00000u);           // di = -1
+            const bool up = (upm >> j) & 1ull;
+            const uint32_t a1 = rl(D[q][1].x, j), b1 = rl(D[q][0].z, j);
+            const uint32_t a2 = rl(D[q][1].y, j), b2 = rl(D[q][0].w, j);
+            const uint32_t ao = rl(D[q][1].w, j), bo = rl(D[q][1].z, j);
+            uint32_t dk1 = up ? a1 : b1;
+            uint32_t dk2 = up ? a2 : b2;
+            uint32_t ob = up ? ao : bo;
+            if (!up && !((dnm >> j) & 1ull)) {                 // rare: |di| > 1
+                const uint4 f = pll_full(fc, rl(D[q][0].x, j), rl(v, j) >> 22, sb + base + j);
+                dk1 = __builtin_amdgcn_readfirstlane(f.x);
+                dk2 = __builtin_amdgcn_readfirstlane(f.y);
+                ob = __builtin_amdgcn_readfirstlane(f.z);
+            }
+            n_rep++;
+            pout = lane == j ? ob : pout;
+            PM |= 1ull << j;
+            K = __builtin_amdgcn_readfirstlane(K + dk2 - (uint32_t)j * dk1);   // scalar state
+            DD = __builtin_amdgcn_readfirstlane(DD + dk1);
+            ldd = (uint32_t)lane * DD;
+            M &= (~0ull << j) << 1;
+        }
+        if (PM != 0 && ((PM >> lane) & 1ull)) yb[base + lane] = __uint_as_float(pout);
+        K += (uint32_t)nvalid * DD;
+        if (!FULL && nvalid < 64) return;
+    }
+}
+
+// Wave 0 walks block c; waves 1-7 store block c+1 (fetched into registers
+// during the previous block) into the other LDS buffer and fetch block c+2.
+__global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, long nblk, CandBuf cb,
+                                                           float* __restrict__ y)
+{
     __shared__ WalkBuf buf[2];
     const int tid = threadIdx.x;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: keeps the walk on SALU
     const int lane = tid & 63;
-    for (int i = tid; i < 1024; i += 256) tab[i] = in.table[i];
-    walk_load(buf[0], cb, 0, n, tid, 256);
+    const int lt = tid - 64;
+    LoadRegs lr;
+    if (wave != 0) {
+        walk_fetch(lr, cb, 0, lt);
+        walk_store(buf[0], lr, lt);
+        if (nblk > 1) walk_fetch(lr, cb, 1, lt);
+    }
     __syncthreads();
-    const float alpha = st->alpha, beta = st->beta;
-    uint32_t th_t = st->theta, d_t = st->dtheta;      // true state at the current chunk start
-    for (long c = 0; c < nch; c++) {
-        const int cur = (int)(c & 1);
+    FullCtx fc;
+    fc.x0 = in.x0;
+    fc.x = in.x;
+    fc.hist = in.hist;
+    fc.table = in.table;
+    fc.m = in.m;
+    fc.costas = in.costas;
+    fc.alpha = st->alpha;
+    fc.beta = st->beta;
+    fc.mod_index = in.mod_index;
+    uint32_t th_t = st->theta, d_t = st->dtheta;      // true state at the current block start
+    const int dbgw = __builtin_amdgcn_readfirstlane(cb.dbg);
+    unsigned long long n_rep = 0, cyc_walk = 0, cyc_wait = 0;
+    for (long c = 0; c < nblk; c++) {
+        const unsigned long long t0 = wall_clock64();
         if (wave != 0) {
-            if (c + 1 < nch) walk_load(buf[cur ^ 1], cb, c + 1, n, tid - 64, 192);
+            if (c + 1 < nblk) {
+                walk_store(buf[(c + 1) & 1], lr, lt);
+                if (c + 2 < nblk) walk_fetch(lr, cb, c + 2, lt);
+            }
         } else {
-            const WalkBuf& b = buf[cur];
-            const long s0 = c * kChunk;
-            const int cnt = (int)min((long)kChunk, n - s0);
-            uint32_t dth = th_t - b.cs[0];            // offset of the true trajectory (exact, mod 2^32)
-            uint32_t dd = d_t - b.cs[1];
-            int p = 0;                                // dth is the offset at local sample p
-            for (int wb = 0; wb < cnt; wb += 64) {
-                const int nl = wb + lane;
-                const bool valid = nl < cnt;
-                const uint32_t thc = valid ? b.th[nl] : 0u;
-                const uint32_t ic = tidx(thc);
-                while (true) {
-                    const uint32_t pred = thc + dth + (uint32_t)(nl - p) * dd;
-                    const bool mis = valid && nl >= p && tidx(pred) != ic;
-                    const unsigned long long mask = __ballot(mis);
-                    if (mask == 0) break;
-                    const int j = __ffsll((long long)mask) - 1;
-                    const int ns = wb + j;                                   // local sample to repair
-                    const uint32_t thn = __builtin_amdgcn_readlane(thc, j);
-                    const uint32_t dthn = dth + (uint32_t)(ns - p) * dd;     // offset at ns
-                    const uint32_t it = tidx(thn + dthn), icn = tidx(thn);
-                    const uint32_t di = (it - icn) & 0x3ffu;
-                    uint32_t dk1, dk2;
-                    float out;
-                    if (di == 0x3ffu) {
-                        dk1 = b.dk[0][ns];
-                        dk2 = b.dk[1][ns];
-                        out = b.om[0][ns];
-                    } else if (di == 1u) {
-                        dk1 = b.dk[2][ns];
-                        dk2 = b.dk[3][ns];
-                        out = b.om[1][ns];
-                    } else {                                                 // rare: full step
-                        const float2 u0 = in.x0[s0 + ns], u1 = x1_at(in, s0 + ns);
-                        const Kick kt = pll_eval(tab, it, u0, u1, alpha, beta, in.mod_index, in.costas);
-                        const Kick kc = pll_eval(tab, icn, u0, u1, alpha, beta, in.mod_index, in.costas);
-                        dk1 = kt.k1 - kc.k1;
-                        dk2 = kt.k2 - kc.k2;
-                        out = kt.out;
+            const WalkBuf& b = buf[c & 1];
+            const long s0 = c * kBlk;
+            const int cnt = (int)min((long)kBlk, n - s0);
+            float* yb = y + s0;
+            // Offset of the true trajectory from the candidate (exact, mod 2^32):
+            // at local sample base + l of the current lane-block, dtheta = K + l*DD.
+            uint32_t K = th_t - b.cs[0];
+            uint32_t DD = d_t - b.cs[1];
+            uint32_t ldd = (uint32_t)lane * DD;
+            uint4 D0[4][2], D1[4][2];
+            load_sub(D0, b, 0, lane);
+            int last = 0;
+            if (cnt == kBlk) {
+#pragma unroll
+                for (int sub = 0; sub < kSub; sub++) {
+                    if (sub > 0) {                                  // next candidate chunk: rebase the offset
+                        K = b.ce[2 * sub - 2] + K - b.cs[2 * sub];
+                        DD = b.ce[2 * sub - 1] + DD - b.cs[2 * sub + 1];
+                        ldd = (uint32_t)lane * DD;
                     }
-                    if (lane == 0) y[s0 + ns] = out;
-                    dth = dthn + dd + dk1 + dk2;
-                    dd = dd + dk1;
-                    p = ns + 1;
+                    if (sub & 1) {
+                        if (sub + 1 < kSub) load_sub(D0, b, sub + 1, lane);
+                        walk_sub<true>(D1, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, dbgw);
+                    } else {
+                        if (sub + 1 < kSub) load_sub(D1, b, sub + 1, lane);
+                        walk_sub<true>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, dbgw);
+                    }
+                }
+                last = kSub - 1;
+            } else {
+                for (int sub = 0; sub * kCand < cnt; sub++) {
+                    if (sub > 0) {
+                        K = b.ce[2 * sub - 2] + K - b.cs[2 * sub];
+                        DD = b.ce[2 * sub - 1] + DD - b.cs[2 * sub + 1];
+                        ldd = (uint32_t)lane * DD;
+                    }
+                    load_sub(D0, b, sub, lane);
+                    walk_sub<false>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, dbgw);
+                    last = sub;
                 }
             }
-            // true state at the chunk end = candidate end + offset propagated to cnt
-            th_t = b.ce[0] + dth + (uint32_t)(cnt - p) * dd;
-            d_t = b.ce[1] + dd;
+            // true state at the block end = candidate end + offset at cnt
+            th_t = b.ce[2 * last] + K;
+            d_t = b.ce[2 * last + 1] + DD;
         }
+        const unsigned long long t1 = wall_clock64();
         __syncthreads();
+        const unsigned long long t2 = wall_clock64();
+        cyc_walk += t1 - t0;
+        cyc_wait += t2 - t1;
     }
     if (tid == 0) {
         st->theta = th_t;
         st->dtheta = d_t;
+        cb.stats[0] = n_rep;
+        cb.stats[1] = 0;
+        cb.stats[2] = cyc_walk;
+        cb.stats[3] = cyc_wait;
     }
 }
 
@@ -285,9 +453,15 @@ __global__ void k_delay_hist(const float2* __restrict__ x, const float2* __restr
 
 size_t pll_scratch_bytes(size_t n)
 {
-    const size_t nch = (n + kChunk - 1) / kChunk;
-    const size_t npad = nch * kChunk;
-    return npad * 4 * 7 + nch * 16 + 256;
+    const size_t nblk = (n + kBlk - 1) / kBlk;
+    const size_t npad = nblk * kBlk;
+    return npad * 32 + nblk * kSub * 16 + 256;
+}
+
+size_t pll_stats_offset(size_t n)
+{
+    const size_t nblk = (n + kBlk - 1) / kBlk;
+    return nblk * kBlk * 32 + nblk * kSub * 16;
 }
 
 void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_out, int m, size_t n, AmpState* st,
@@ -306,19 +480,21 @@ void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_ou
         hipLaunchKernelGGL(k_pll_seq, dim3(1), dim3(256), 0, s, in, (long)n, st, y);
         LDSP_HIP(hipGetLastError());
     } else {
-        const long nch = (long)((n + kChunk - 1) / kChunk);
+        const long nblk = (long)((n + kBlk - 1) / kBlk);
+        const long nchc = (long)((n + kCand - 1) / kCand);
         CandBuf cb;
-        cb.npad = nch * kChunk;
+        cb.npad = nblk * kBlk;
         char* p = (char*)scratch;
-        cb.th = (uint32_t*)p;
-        cb.dk = (uint32_t*)(p + (size_t)cb.npad * 4);
-        cb.om = (float*)(p + (size_t)cb.npad * 4 * 5);
-        cb.cs = (uint32_t*)(p + (size_t)cb.npad * 4 * 7);
-        cb.ce = cb.cs + 2 * nch;
-        hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((nch + 63) / 64)), dim3(64), 0, s, in, (long)n,
-                           (const AmpState*)st, nch, cb, y);
+        cb.rec = (uint4*)p;
+        cb.cs = (uint32_t*)(p + (size_t)cb.npad * 32);
+        cb.ce = cb.cs + 2 * nblk * kSub;
+        cb.stats = (unsigned long long*)(p + pll_stats_offset(n));
+        static const int dbg_mode = std::getenv("LDSP_DEBUG_PLL_MODE") ? std::atoi(std::getenv("LDSP_DEBUG_PLL_MODE")) : 0;
+        cb.dbg = dbg_mode;
+        hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((nchc + 63) / 64)), dim3(64), 0, s, in, (long)n,
+                           (const AmpState*)st, nchc, cb, y);
         LDSP_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_pll_walk, dim3(1), dim3(256), 0, s, in, (long)n, st, nch, cb, y);
+        hipLaunchKernelGGL(k_pll_walk, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
         LDSP_HIP(hipGetLastError());
     }
     // delay-line history for the next call (m samples); k_pll_* read the old one

@@ -102,6 +102,7 @@ struct AmpState {         // device-resident PLL state
 // m = Re(v1)/mod (carrier) or the final output (Costas) to y.  scratch (of
 // pll_scratch_bytes(n)) enables the chunk-parallel exact path (k_pll.hip).
 size_t pll_scratch_bytes(size_t n);
+size_t pll_stats_offset(size_t n);     // 4 x u64 walker counters inside the scratch (debug)
 void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_out, int m, size_t n,
                   AmpState* st, const float* table, float mod_index, int costas, float* y, void* scratch,
                   hipStream_t s);
