@@ -32,7 +32,12 @@
  *  - NCO: 1024-entry sine table, index ((theta + 2^21) >> 22) & 1023;
  *  - dot products: the portable C dotprod (sequential accumulation from the
  *    oldest sample, no FMA); SIMD builds of liquid sum in another order;
- *  - transcendentals inside feedback loops: ora_math.h (fdlibm algorithms).
+ *  - transcendentals inside feedback loops: ora_math.h (fdlibm algorithms);
+ *  - complex division in the filter designs: C's `/` on _Complex operands,
+ *    i.e. libgcc __divsc3 / __divdc3.  This library is linked by gcc 11, whose
+ *    static libgcc implements Smith's method; newer libgcc_s (also present in
+ *    the image) uses a scaled variant that moves some cheby2 poles by 1 ulp.
+ *    The product pins Smith's method explicitly (csrc/cplx_c.c).
  *
  * Build flags: -ffp-contract=off (liquid's x86-64 baseline build has no FMA),
  * no -ffast-math.

@@ -25,6 +25,24 @@ using cf = std::complex<float>;
 using cd = std::complex<double>;
 static constexpr double kPi = 3.14159265358979323846;
 
+// Complex division exactly as C's `/` on _Complex operands (cplx_c.c, compiled
+// as C): C++ compilers lower std::complex division with another algorithm
+// (1-ulp differences in the cheby2 poles / zeros).
+extern "C" void ldsp_cdivf(float ar, float ai, float br, float bi, float* out);
+extern "C" void ldsp_cdivd(double ar, double ai, double br, double bi, double* out);
+static inline cf cdiv(cf x, cf y)
+{
+    float r[2];
+    ldsp_cdivf(x.real(), x.imag(), y.real(), y.imag(), r);
+    return cf(r[0], r[1]);
+}
+static inline cd cdiv(cd x, cd y)
+{
+    double r[2];
+    ldsp_cdivd(x.real(), x.imag(), y.real(), y.imag(), r);
+    return cd(r[0], r[1]);
+}
+
 // liquid math.gamma.c liquid_lngammaf
 static float lngammaf_(float z)
 {
@@ -165,16 +183,16 @@ void cheby2_azpk(unsigned int n, float es, std::vector<cf>& za, std::vector<cf>&
     const unsigned int r = n % 2, L = (n - r) / 2;
     for (unsigned int i = 0; i < L; i++) {
         const float th = theta_pole(i, n);
-        pa.push_back(cf(1.0f, 0.0f) / ellipse_point(a, b, th, false));
-        pa.push_back(cf(1.0f, 0.0f) / ellipse_point(a, b, th, true));
+        pa.push_back(cdiv(cf(1.0f, 0.0f), ellipse_point(a, b, th, false)));
+        pa.push_back(cdiv(cf(1.0f, 0.0f), ellipse_point(a, b, th, true)));
     }
     if (r) pa.push_back(cf(-1.0f / a, 0.0f));
     for (unsigned int i = 0; i < L; i++) {
         const float th = (float)(0.5 * kPi * (double)(2 * (i + 1) - 1) / (double)(float)n);
         const float c = cosf(th);
         const cf jc(0.0f * c, 1.0f * c);               // _Complex_I*cosf(theta)
-        za.push_back(cf(-1.0f, 0.0f) / jc);
-        za.push_back(cf(1.0f, 0.0f) / jc);
+        za.push_back(cdiv(cf(-1.0f, 0.0f), jc));
+        za.push_back(cdiv(cf(1.0f, 0.0f), jc));
     }
 }
 
@@ -195,7 +213,7 @@ cf bilin(cf z)
 {
     const cd num(1.0 + (double)z.real(), (double)z.imag());
     const cd den(1.0 - (double)z.real(), -(double)z.imag());
-    const cd q = num / den;
+    const cd q = cdiv(num, den);
     return cf((float)q.real(), (float)q.imag());
 }
 
@@ -211,7 +229,7 @@ void bilinear(const std::vector<cf>& za, const std::vector<cf>& pa, cf ka, float
         pd[i] = bilin(pa[i] * m);
         const cd a(1.0 - (double)pd[i].real(), -(double)pd[i].imag());
         const cd b(1.0 - (double)zd[i].real(), -(double)zd[i].imag());
-        const cd g = cd((double)G.real(), (double)G.imag()) * (a / b);
+        const cd g = cd((double)G.real(), (double)G.imag()) * cdiv(a, b);
         G = cf((float)g.real(), (float)g.imag());
     }
     kd = G;
