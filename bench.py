@@ -78,6 +78,35 @@ class AMRadio:
         return x
 
 
+def timed_steps(step, steps, warmup, sync, barrier):
+    """W untimed warmup steps, then exactly K steps bracketed by a barrier and a
+    device synchronize on both sides; returns this rank's wall time (s)."""
+    for _ in range(warmup):
+        step(None)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def reduce_max(elapsed, device):
+    """Max of the per-rank wall times (the job takes as long as its slowest rank)."""
+    import torch.distributed as tdist
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_value(world, n_per_rank, steps, elapsed):
+    """Whole-job throughput: IQ samples all ranks processed / max wall time (Msamples/s)."""
+    return world * n_per_rank * steps / elapsed / 1e6
+
+
 def cpu_baseline(n_iq, seconds=10.0):
     """Time the CPU restatement (oracle/, -O3, single thread) on a bounded sample."""
     from oracle import oracle as O
@@ -129,33 +158,23 @@ def main():
     radio = AMRadio(L)
     nst = len(radio.stages())
 
-    for _ in range(args.warmup):
-        radio(x)
-    torch.cuda.synchronize()
-
     events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nst)]
               for _ in range(args.steps)]
+    out = {}
+
+    def step(k):
+        out["y"] = radio(x, events[k] if k is not None else None)
+
+    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize,
+                          tdist.barrier if dist else (lambda: None))
     if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    out = None
-    for k in range(args.steps):
-        out = radio(x, events[k])
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = reduce_max(elapsed, device)
+    out = out["y"]
 
     stage_ms = {name: float(np.mean([events[k][i][0].elapsed_time(events[k][i][1]) for k in range(args.steps)]))
                 for i, (name, _) in enumerate(radio.stages())}
     n_pcm = int(out.numel())
-    total = world * args.n * args.steps
-    value = total / elapsed / 1e6
+    value = aggregate_value(world, args.n, args.steps, elapsed)
 
     # algorithmic bytes per stage launch (read input once, write output once)
     r = 48000 / 2000000
