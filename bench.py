@@ -139,6 +139,7 @@ def main():
     ap.add_argument("--n", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-components", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,25 +164,41 @@ def main():
     out = {}
 
     def step(k):
+        if k == 0:
+            L._profile_reset()                 # per-kernel HIP events over exactly the timed steps
+            L._profile_enable(True)
         out["y"] = radio(x, events[k] if k is not None else None)
 
     elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize,
                           tdist.barrier if dist else (lambda: None))
+    L._profile_enable(False)
+    kprof = L._profile_report()
     if dist:
         elapsed = reduce_max(elapsed, device)
-    out = out["y"]
+    y = out["y"]
 
     stage_ms = {name: float(np.mean([events[k][i][0].elapsed_time(events[k][i][1]) for k in range(args.steps)]))
                 for i, (name, _) in enumerate(radio.stages())}
-    n_pcm = int(out.numel())
+    n_pcm = int(y.numel())
     value = aggregate_value(world, args.n, args.steps, elapsed)
 
-    # algorithmic bytes per stage launch (read input once, write output once)
-    r = 48000 / 2000000
-    alg_bytes = {"iir": 16 * args.n, "resamp": 8 * args.n + 8 * n_pcm, "agc": 16 * n_pcm,
-                 "ampmodem": 8 * n_pcm + 4 * n_pcm, "deemph": 8 * n_pcm}
-    dom = max(stage_ms, key=stage_ms.get)
-    achieved = alg_bytes[dom] / (stage_ms[dom] * 1e-3) / 1e9
+    # Algorithmic bytes per launch (read the stage input once, write
+    # its output once; complex64 = 8 B, float32 = 4 B).  Multi-kernel stages
+    # attribute the stage minimum to the kernel that produces the stage output.
+    n = args.n
+    alg = {"k_iir_scan_local": 8 * n, "k_iir_scan_carry": 0, "k_iir_scan_final": 16 * n,
+           "k_resamp": 8 * n + 8 * n_pcm, "k_agc_chunks": 16 * n_pcm, "k_agc_verify": 0,
+           "k_fir_exact": 8 * n_pcm + 8 * n_pcm, "k_pll_cand": 12 * n_pcm, "k_pll_walk": 12 * n_pcm,
+           "k_iir_spec_chunks": 8 * n_pcm, "k_iir_spec_verify": 0, "k_delay_hist": 0}
+    kernels = {}
+    for name, (calls, tot) in kprof.items():
+        per = tot / calls
+        ab = alg.get(name, 0)
+        kernels[name] = {"calls_per_step": round(calls / args.steps, 2), "ms": round(per, 4),
+                         "alg_GBs": round(ab / (per * 1e-3) / 1e9, 2) if ab else None}
+    dom = max(kprof, key=lambda k: kprof[k][1])
+    dom_ms = kprof[dom][1] / kprof[dom][0]
+    achieved = alg.get(dom, 0) / (dom_ms * 1e-3) / 1e9
     res = {
         "metric": "Msamples/s on AM chain (IIR->resample->AGC->demod), 2 MS/s IQ; HBM GB/s vs roofline",
         "value": round(value, 3),
@@ -199,16 +216,70 @@ def main():
                                "-> de-emphasis), one independent channel per GPU",
                    "samples_per_step_per_gpu": args.n, "iq_rate": 2000000, "pcm_rate": 48000,
                    "pcm_samples_per_step": n_pcm, "parallelism": f"channel-per-gpu x{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None},
+        "roofline": {"bound": "hbm", "kernel": dom, "ms_per_launch": round(dom_ms, 4),
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "note": "alg bytes = 12 B per PCM sample (AmpModem in + out); the PLL recurrence is "
+                             "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else ""},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+        "kernels": kernels,
     }
+    if rank == 0 and world == 1 and not args.no_components:
+        res["components"] = components(L, device)
     if rank == 0 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.n, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def components(L, device, reps=5):
+    """The north-star kernel (127-tap ComplexFIRFilter on 64 Mi samples, target
+    >= 50 % of the HBM roofline) and BASELINE config 3 (NCO.mix_down + 255-tap
+    ComplexFIRFilter on 256 Mi samples), per-kernel HIP-event times."""
+    g = torch.Generator(device=device)
+    g.manual_seed(1)
+
+    def kaiser(n, fc, As):
+        beta = 0.1102 * (As - 8.7)
+        t = np.arange(n) - (n - 1) / 2
+        r = 2 * t / n
+        return (np.sinc(2 * fc * t) * np.i0(beta * np.sqrt(1 - r * r)) / np.i0(beta)).astype(np.float32)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        L._profile_reset()
+        L._profile_enable(True)
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        L._profile_enable(False)
+        return {k: v[1] / v[0] for k, v in L._profile_report().items()}
+
+    out = {}
+    n = 64 << 20
+    xs = torch.complex(torch.randn(n, generator=g, device=device), torch.randn(n, generator=g, device=device))
+    f = L.ComplexFIRFilter(kaiser(127, 0.1, 60.0))
+    ms = timed(lambda: f(xs))["k_fir_fast"]
+    out["fir127_64Mi"] = {"kernel": "k_fir_fast", "ms": round(ms, 4), "GBs": round(16 * n / ms / 1e6, 1),
+                          "hbm_frac": round(16 * n / ms / 1e6 / HBM_PEAK_GBS, 4),
+                          "TFLOPs": round(4 * 127 * n / ms / 1e9, 2),
+                          "valu_frac": round(4 * 127 * n / ms / 1e9 / FP32_PEAK_TFLOPS, 4)}
+    del xs
+    n = 256 << 20
+    xs = torch.complex(torch.randn(n, generator=g, device=device), torch.randn(n, generator=g, device=device))
+    nco = L.NCO("nco")
+    nco.freq = float(2 * np.pi * 0.05)
+    f2 = L.ComplexFIRFilter(kaiser(255, 0.05, 60.0))
+    t = timed(lambda: f2(nco.mix_down(xs)))
+    out["nco_fir255_256Mi"] = {"nco_ms": round(t["k_nco_mix"], 4), "fir_ms": round(t["k_fir_fast"], 4),
+                               "nco_GBs": round(16 * n / t["k_nco_mix"] / 1e6, 1),
+                               "fir_TFLOPs": round(4 * 255 * n / t["k_fir_fast"] / 1e9, 2),
+                               "Msamples_s": round(n / (t["k_nco_mix"] + t["k_fir_fast"]) / 1e3, 1)}
+    del xs
+    return out
 
 
 if __name__ == "__main__":

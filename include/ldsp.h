@@ -60,6 +60,13 @@ int ldsp_stream_synchronize(void *stream);
  * a, b, y are device pointers of n floats. */
 int ldsp_debug_math_eval(int fn, const float *a, const float *b, float *y, size_t n, void *stream);
 
+/* Per-kernel device timing (no reference counterpart; measurement support for
+ * bench.py).  While enabled every kernel launch is bracketed by a HIP event
+ * pair on its stream; the report lists "name calls total_ms" lines. */
+int ldsp_profile_enable(int on);
+int ldsp_profile_reset(void);
+int ldsp_profile_report(char *buf, size_t cap, size_t *len);
+
 /* ------------------------------------------------------------------------
  * FIR filter: firfilt_rrrf (cplx=0) / firfilt_crcf (cplx=1), real taps.
  * Replaces RealFIRFilter (src/firfilter.hpp:13-35, firfilt_rrrf_create /

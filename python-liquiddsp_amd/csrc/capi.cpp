@@ -6,6 +6,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -523,7 +524,99 @@ static int guard(F&& fn)
 
 #define NONNULL(p) LDSP_REQUIRE((p) != nullptr, #p " must not be NULL")
 
+// ---------------------------------------------------------------- per-kernel timing
+namespace ldsp {
+namespace prof {
+namespace {
+std::atomic<bool> g_on{false};
+std::mutex g_mu;
+struct Pending {
+    const char* name;
+    hipEvent_t a, b;
+};
+std::vector<Pending> g_pending;
+std::vector<std::pair<std::string, std::pair<long, double>>> g_done;   // name -> (calls, total ms)
+
+void drain_locked()
+{
+    for (auto& r : g_pending) {
+        float ms = 0.0f;
+        if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&ms, r.a, r.b);
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+        auto it = std::find_if(g_done.begin(), g_done.end(), [&](const auto& e) { return e.first == r.name; });
+        if (it == g_done.end()) g_done.push_back({r.name, {1, (double)ms}});
+        else {
+            it->second.first++;
+            it->second.second += ms;
+        }
+    }
+    g_pending.clear();
+}
+} // namespace
+
+bool enabled() { return g_on.load(std::memory_order_relaxed); }
+
+Scope::Scope(hipStream_t s_, const char* n) : s(s_), name(n)
+{
+    if (!enabled()) return;
+    if (hipEventCreate(&a) != hipSuccess || hipEventRecord(a, s) != hipSuccess) a = nullptr;
+}
+
+Scope::~Scope()
+{
+    if (!a) return;
+    hipEvent_t b = nullptr;
+    if (hipEventCreate(&b) != hipSuccess || hipEventRecord(b, s) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_pending.push_back({name, a, b});
+    if (g_pending.size() > 4096) drain_locked();
+}
+} // namespace prof
+} // namespace ldsp
+
 extern "C" {
+
+int ldsp_profile_enable(int on)
+{
+    ldsp::prof::g_on.store(on != 0);
+    return LDSP_OK;
+}
+
+int ldsp_profile_reset(void)
+{
+    return guard([&] {
+        std::lock_guard<std::mutex> lk{ldsp::prof::g_mu};
+        ldsp::prof::drain_locked();
+        ldsp::prof::g_done.clear();
+    });
+}
+
+int ldsp_profile_report(char* buf, size_t cap, size_t* len)
+{
+    return guard([&] {
+        NONNULL(len);
+        std::string out;
+        {
+            std::lock_guard<std::mutex> lk{ldsp::prof::g_mu};
+            ldsp::prof::drain_locked();
+            char line[256];
+            for (const auto& e : ldsp::prof::g_done) {
+                std::snprintf(line, sizeof(line), "%s %ld %.6f\n", e.first.c_str(), e.second.first, e.second.second);
+                out += line;
+            }
+        }
+        *len = out.size();
+        if (buf && cap > 0) {
+            const size_t m = std::min(cap - 1, out.size());
+            std::memcpy(buf, out.data(), m);
+            buf[m] = 0;
+        }
+    });
+}
 
 const char* ldsp_last_error(void) { return g_last_error.c_str(); }
 int ldsp_version(void) { return 100; }

@@ -248,25 +248,37 @@ __global__ void k_math_eval(int fn, const float* __restrict__ a, const float* __
 void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_agc_seq, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, (float2*)y, status);
+    {
+        LDSP_PROF(s, "k_agc_seq");
+        hipLaunchKernelGGL(k_agc_seq, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, (float2*)y, status);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
 void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_agc_chunks, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, (const float2*)x,
-                       (long)n, (const AgcState*)st, p.C, p.W, p.nchunks, (unsigned*)p.scratch, (float2*)y, status);
+    {
+        LDSP_PROF(s, "k_agc_chunks");
+        hipLaunchKernelGGL(k_agc_chunks, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, (const float2*)x,
+                           (long)n, (const AgcState*)st, p.C, p.W, p.nchunks, (unsigned*)p.scratch, (float2*)y, status);
+    }
     LDSP_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, p.nchunks,
-                       (unsigned*)p.scratch, (float2*)y, status);
+    {
+        LDSP_PROF(s, "k_agc_verify");
+        hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, p.nchunks,
+                           (unsigned*)p.scratch, (float2*)y, status);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
 void math_eval(int fn, const float* a, const float* b, float* y, size_t n, hipStream_t s)
 {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_math_eval, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fn, a, b, y, (long)n);
+    {
+        LDSP_PROF(s, "k_math_eval");
+        hipLaunchKernelGGL(k_math_eval, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fn, a, b, y, (long)n);
+    }
     LDSP_HIP(hipGetLastError());
 }
 

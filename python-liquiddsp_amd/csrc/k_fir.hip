@@ -194,8 +194,11 @@ void fir_fast_t(const void* x, const void* hist, void* hist_out, size_t n, const
         LDSP_HIP(hipFuncSetAttribute((const void*)k_fir_fast<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
     const unsigned grid = (unsigned)((n + kTile - 1) / kTile);
-    hipLaunchKernelGGL(k_fir_fast<T>, dim3(grid), dim3(kThreads), lds, s, (const T*)x, (const T*)hist,
-                       (T*)hist_out, (long)n, taps, L, scale, (T*)y);
+    {
+        LDSP_PROF(s, "k_fir_fast");
+        hipLaunchKernelGGL(k_fir_fast<T>, dim3(grid), dim3(kThreads), lds, s, (const T*)x, (const T*)hist,
+                           (T*)hist_out, (long)n, taps, L, scale, (T*)y);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
@@ -208,16 +211,22 @@ void fir_exact_t(const void* x, const void* hist, void* hist_out, size_t n, cons
         LDSP_HIP(hipFuncSetAttribute((const void*)k_fir_exact<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
     const unsigned grid = (unsigned)((n + kExactOut - 1) / kExactOut);
-    hipLaunchKernelGGL(k_fir_exact<T>, dim3(grid), dim3(kThreads), lds, s, (const T*)x, (const T*)hist,
-                       (T*)hist_out, (long)n, taps, L, scale, (T*)y);
+    {
+        LDSP_PROF(s, "k_fir_exact");
+        hipLaunchKernelGGL(k_fir_exact<T>, dim3(grid), dim3(kThreads), lds, s, (const T*)x, (const T*)hist,
+                           (T*)hist_out, (long)n, taps, L, scale, (T*)y);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
 template <typename T>
 void fir_hist_t(const void* x, const void* hist, void* hist_out, size_t n, int L, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_fir_hist_only<T>, dim3(1), dim3(256), 0, s, (const T*)x, (const T*)hist, (T*)hist_out,
-                       (long)n, L - 1);
+    {
+        LDSP_PROF(s, "k_fir_hist_only");
+        hipLaunchKernelGGL(k_fir_hist_only<T>, dim3(1), dim3(256), 0, s, (const T*)x, (const T*)hist, (T*)hist_out,
+                           (long)n, L - 1);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
@@ -327,12 +336,18 @@ void resamp(bool cplx, const void* x, const void* hist, void* hist_out, size_t n
         if (lds > 64 * 1024)
             LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)lds));
-        hipLaunchKernelGGL(k_resamp<true>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
+        {
+            LDSP_PROF(s, "k_resamp");
+            hipLaunchKernelGGL(k_resamp<true>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
+        }
     } else {
         if (lds > 64 * 1024)
             LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)lds));
-        hipLaunchKernelGGL(k_resamp<false>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
+        {
+            LDSP_PROF(s, "k_resamp");
+            hipLaunchKernelGGL(k_resamp<false>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
+        }
     }
     LDSP_HIP(hipGetLastError());
 }
@@ -397,11 +412,17 @@ void nco_mix(const void* x, void* y, size_t n, uint32_t theta0, uint32_t dtheta,
     if (n == 0) return;
     const unsigned grid = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
     if (type == 0)
-        hipLaunchKernelGGL(k_nco_mix, dim3(grid), dim3(256), 0, s, (const float2*)x, (float2*)y, (long)n, theta0,
-                           dtheta, table, (int)down);
+        {
+            LDSP_PROF(s, "k_nco_mix");
+            hipLaunchKernelGGL(k_nco_mix, dim3(grid), dim3(256), 0, s, (const float2*)x, (float2*)y, (long)n, theta0,
+                               dtheta, table, (int)down);
+        }
     else
-        hipLaunchKernelGGL(k_vco_mix, dim3(grid), dim3(256), 0, s, (const float2*)x, (float2*)y, (long)n, theta0,
-                           dtheta, (int)down);
+        {
+            LDSP_PROF(s, "k_vco_mix");
+            hipLaunchKernelGGL(k_vco_mix, dim3(grid), dim3(256), 0, s, (const float2*)x, (float2*)y, (long)n, theta0,
+                               dtheta, (int)down);
+        }
     LDSP_HIP(hipGetLastError());
 }
 

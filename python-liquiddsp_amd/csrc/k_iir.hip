@@ -475,8 +475,11 @@ void launch_carry(int ncomp, const IirScanPlan& p, const double* state64, hipStr
     if (lds > 64 * 1024)
         LDSP_HIP(hipFuncSetAttribute((const void*)k_iir_scan_carry<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
-    hipLaunchKernelGGL(k_iir_scan_carry<D>, dim3(1), dim3(1024), lds, s, ncomp, p.nchunks, p.G, p.levels, p.AC,
-                       p.AG, state64, p.local, p.carry);
+    {
+        LDSP_PROF(s, "k_iir_scan_carry");
+        hipLaunchKernelGGL(k_iir_scan_carry<D>, dim3(1), dim3(1024), lds, s, ncomp, p.nchunks, p.G, p.levels, p.AC,
+                           p.AG, state64, p.local, p.carry);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
@@ -486,8 +489,11 @@ void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state,
 {
     if (n == 0) return;
     LDSP_REQUIRE(d.sos ? d.nsos <= kMaxSos : d.nv <= kMaxTf, "iir: filter order too high for the GPU kernels");
-    hipLaunchKernelGGL(k_iir_seq, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, cplx ? 2 : 1, state,
-                       (float*)y);
+    {
+        LDSP_PROF(s, "k_iir_seq");
+        hipLaunchKernelGGL(k_iir_seq, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, cplx ? 2 : 1, state,
+                           (float*)y);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
@@ -497,11 +503,17 @@ void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state
     if (n == 0) return;
     const int ncomp = cplx ? 2 : 1;
     const long work = p.nchunks * ncomp;
-    hipLaunchKernelGGL(k_iir_spec_chunks, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, s, d, (const float*)x,
-                       (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks, (float*)p.scratch, (float*)y);
+    {
+        LDSP_PROF(s, "k_iir_spec_chunks");
+        hipLaunchKernelGGL(k_iir_spec_chunks, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, s, d, (const float*)x,
+                           (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks, (float*)p.scratch, (float*)y);
+    }
     LDSP_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_iir_spec_verify, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, ncomp, p.C, p.W,
-                       p.nchunks, (float*)p.scratch, state, (float*)y);
+    {
+        LDSP_PROF(s, "k_iir_spec_verify");
+        hipLaunchKernelGGL(k_iir_spec_verify, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, ncomp, p.C, p.W,
+                           p.nchunks, (float*)p.scratch, state, (float*)y);
+    }
     LDSP_HIP(hipGetLastError());
 }
 
@@ -512,8 +524,11 @@ void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* stat
     LDSP_REQUIRE(d.D >= 1 && d.D <= kMaxD, "iir: state dimension too large for the scan kernels");
     const int ncomp = cplx ? 2 : 1;
     const unsigned g = (unsigned)((p.nchunks + 255) / 256);
-    hipLaunchKernelGGL(k_iir_scan_local, dim3(g), dim3(256), 0, s, d, (const float*)x, (long)n, ncomp, p.C,
-                       p.nchunks, p.local);
+    {
+        LDSP_PROF(s, "k_iir_scan_local");
+        hipLaunchKernelGGL(k_iir_scan_local, dim3(g), dim3(256), 0, s, d, (const float*)x, (long)n, ncomp, p.C,
+                           p.nchunks, p.local);
+    }
     LDSP_HIP(hipGetLastError());
     switch (d.D) {
     case 1: launch_carry<1>(ncomp, p, state64, s); break;
@@ -531,8 +546,11 @@ void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* stat
     default:
         throw Error(LDSP_EUNSUP, "iir: unsupported state dimension for the scan kernels");
     }
-    hipLaunchKernelGGL(k_iir_scan_final, dim3(g), dim3(256), 0, s, d, (const float*)x, (long)n, ncomp, p.C,
-                       p.nchunks, p.carry, state64, (float*)y);
+    {
+        LDSP_PROF(s, "k_iir_scan_final");
+        hipLaunchKernelGGL(k_iir_scan_final, dim3(g), dim3(256), 0, s, d, (const float*)x, (long)n, ncomp, p.C,
+                           p.nchunks, p.carry, state64, (float*)y);
+    }
     LDSP_HIP(hipGetLastError());
 }
 

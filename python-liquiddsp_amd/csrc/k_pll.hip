@@ -477,7 +477,10 @@ void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_ou
     in.mod_index = mod_index;
     in.costas = costas;
     if (n < (size_t)4 * kWarm || scratch == nullptr) {
-        hipLaunchKernelGGL(k_pll_seq, dim3(1), dim3(256), 0, s, in, (long)n, st, y);
+        {
+            LDSP_PROF(s, "k_pll_seq");
+            hipLaunchKernelGGL(k_pll_seq, dim3(1), dim3(256), 0, s, in, (long)n, st, y);
+        }
         LDSP_HIP(hipGetLastError());
     } else {
         const long nblk = (long)((n + kBlk - 1) / kBlk);
@@ -491,15 +494,24 @@ void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_ou
         cb.stats = (unsigned long long*)(p + pll_stats_offset(n));
         static const int dbg_mode = std::getenv("LDSP_DEBUG_PLL_MODE") ? std::atoi(std::getenv("LDSP_DEBUG_PLL_MODE")) : 0;
         cb.dbg = dbg_mode;
-        hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((nchc + 63) / 64)), dim3(64), 0, s, in, (long)n,
-                           (const AmpState*)st, nchc, cb, y);
+        {
+            LDSP_PROF(s, "k_pll_cand");
+            hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((nchc + 63) / 64)), dim3(64), 0, s, in, (long)n,
+                               (const AmpState*)st, nchc, cb, y);
+        }
         LDSP_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_pll_walk, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
+        {
+            LDSP_PROF(s, "k_pll_walk");
+            hipLaunchKernelGGL(k_pll_walk, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
+        }
         LDSP_HIP(hipGetLastError());
     }
     // delay-line history for the next call (m samples); k_pll_* read the old one
-    hipLaunchKernelGGL(k_delay_hist, dim3(1), dim3(64), 0, s, (const float2*)x, (const float2*)hist, (float2*)hist_out,
-                       (long)n, m);
+    {
+        LDSP_PROF(s, "k_delay_hist");
+        hipLaunchKernelGGL(k_delay_hist, dim3(1), dim3(64), 0, s, (const float2*)x, (const float2*)hist, (float2*)hist_out,
+                           (long)n, m);
+    }
     LDSP_HIP(hipGetLastError());
 }
 

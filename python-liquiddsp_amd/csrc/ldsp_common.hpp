@@ -26,6 +26,24 @@ void set_last_error(const std::string& msg);
             throw ::ldsp::Error(LDSP_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// Per-kernel timing (ldsp_profile_enable): a Scope records a HIP event pair on
+// the launch stream around one kernel launch; ldsp_profile_report() resolves
+// them into per-kernel call counts and total device time.  Disabled: one
+// relaxed atomic load per launch.
+namespace prof {
+bool enabled();
+struct Scope {
+    hipEvent_t a = nullptr;
+    hipStream_t s;
+    const char* name;
+    Scope(hipStream_t s_, const char* n);
+    ~Scope();
+};
+} // namespace prof
+#define LDSP_PROF_CAT2(a, b) a##b
+#define LDSP_PROF_CAT(a, b) LDSP_PROF_CAT2(a, b)
+#define LDSP_PROF(stream, name) ::ldsp::prof::Scope LDSP_PROF_CAT(ldsp_prof_, __LINE__)((stream), (name))
+
 #define LDSP_REQUIRE(cond, msg)                                                            \
     do {                                                                                   \
         if (!(cond)) throw ::ldsp::Error(LDSP_EINVAL, (msg));                              \

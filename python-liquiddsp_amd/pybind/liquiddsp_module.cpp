@@ -700,6 +700,28 @@ PYBIND11_MODULE(_liquiddsp, m)
     m.def("_math_eval", [](int fn, uintptr_t a, uintptr_t b, uintptr_t y, size_t n, uintptr_t stream) {
         check(ldsp_debug_math_eval(fn, (const float*)a, (const float*)b, (float*)y, n, (void*)stream));
     });
+    // per-kernel device timing (ldsp_profile_*): {kernel: (calls, total_ms)}
+    m.def("_profile_enable", [](bool on) { check(ldsp_profile_enable(on ? 1 : 0)); });
+    m.def("_profile_reset", [] { check(ldsp_profile_reset()); });
+    m.def("_profile_report", [] {
+        size_t len = 0;
+        check(ldsp_profile_report(nullptr, 0, &len));
+        std::string buf(len + 1, '\0');
+        check(ldsp_profile_report(&buf[0], buf.size(), &len));
+        py::dict d;
+        size_t pos = 0;
+        while (pos < len) {
+            const size_t e = buf.find('\n', pos);
+            const std::string line = buf.substr(pos, (e == std::string::npos ? len : e) - pos);
+            pos = (e == std::string::npos) ? len : e + 1;
+            char name[200];
+            long calls = 0;
+            double ms = 0.0;
+            if (std::sscanf(line.c_str(), "%199s %ld %lf", name, &calls, &ms) == 3)
+                d[py::str(name)] = py::make_tuple(calls, ms);
+        }
+        return d;
+    });
 
     // ---- CIIRFilter / RIIRFilter (wrapper.cpp:30-34, 82-86)
     {
