@@ -49,6 +49,7 @@ extern "C" {
 /* execution modes (exact = bit-identical to the sequential CPU restatement) */
 #define LDSP_MODE_FAST  0
 #define LDSP_MODE_EXACT 1
+#define LDSP_MODE_DIRECT 2   /* FIR only: fast direct form (bitwise invariant to how a stream is cut into calls) */
 
 const char *ldsp_last_error(void);
 int ldsp_version(void);
@@ -85,7 +86,11 @@ int ldsp_firfilt_set_scale(ldsp_firfilt_t q, float scale);
 int ldsp_firfilt_get_scale(ldsp_firfilt_t q, float *scale);
 int ldsp_firfilt_get_length(ldsp_firfilt_t q, unsigned int *n);
 int ldsp_firfilt_get_taps(ldsp_firfilt_t q, float *h);
+/* mode: LDSP_MODE_FAST (default; complex data with 48 <= L <= 1025 taps uses
+ * overlap-save FFT convolution, HBM-bound), LDSP_MODE_DIRECT (register-blocked
+ * direct form), LDSP_MODE_EXACT (liquid dot-product order, bit-identical). */
 int ldsp_firfilt_set_mode(ldsp_firfilt_t q, int mode);
+int ldsp_firfilt_get_mode(ldsp_firfilt_t q, int *mode);
 /* firfilt_*_freqresponse (firfilter.hpp:23-27) */
 int ldsp_firfilt_freqresponse(ldsp_firfilt_t q, float f, float *re, float *im);
 /* firfilt_*_execute_block (firfilter.hpp:29-35): y[i] = scale * sum_k h[k] x[i-k] */

@@ -104,10 +104,54 @@ struct FirObj {
     int mode = LDSP_MODE_FAST;
     int device = -1;
     DevBuf taps_pad, taps_rev, hist[2];
+    DevBuf fft_H, fft_tw;             // overlap-save spectrum (for fft_scale) and twiddles
+    float fft_scale = 0.0f;
+    bool fft_ready = false;
     int cur = 0;
     hipStream_t last = nullptr;
     Staging stg;
     size_t esz() const { return cplx ? 8 : 4; }
+    // FAST on complex data with L in [kFirFftMinTaps, 1025] runs the overlap-save
+    // FFT kernel (HBM-bound); shorter filters and DIRECT use the register-blocked
+    // direct form (VALU-bound at 4 L flop / sample).
+    static constexpr int kFirFftMinTaps = 48;
+    int fft_P() const { return ((int)h.size() - 1 + 63) / 64 * 64; }
+    bool use_fft() const
+    {
+        const int L = (int)h.size();
+        return mode == LDSP_MODE_FAST && cplx && L >= kFirFftMinTaps && fft_P() <= 512;
+    }
+    void prepare_fft()
+    {
+        if (fft_ready && fft_scale == scale) return;
+        const int L = (int)h.size();
+        const int N = k::fir_fft_points(fft_P());
+        std::vector<float> Hf(2 * (size_t)N);
+        for (int f = 0; f < N; f++) {
+            double re = 0.0, im = 0.0;
+            for (int i = 0; i < L; i++) {
+                const double a = -2.0 * M_PI * (double)(((long)f * i) % N) / N;
+                re += (double)h[i] * cos(a);
+                im += (double)h[i] * sin(a);
+            }
+            Hf[2 * f] = (float)(re * (double)scale / N);
+            Hf[2 * f + 1] = (float)(im * (double)scale / N);
+        }
+        // Stockham twiddles exp(-2 pi i r k / (Ns R)), [pass][r-1][k] (kernels.hpp)
+        std::vector<float> tw;
+        const int p512[2][2] = {{8, 8}, {64, 8}}, p1024[2][2] = {{16, 16}, {256, 4}};
+        for (const auto& pr : (N == 512 ? p512 : p1024))
+            for (int r = 1; r < pr[1]; r++)
+                for (int kk = 0; kk < pr[0]; kk++) {
+                    const double a = -2.0 * M_PI * (double)(r * kk) / (double)(pr[0] * pr[1]);
+                    tw.push_back((float)cos(a));
+                    tw.push_back((float)sin(a));
+                }
+        upload(fft_H, Hf, device);
+        upload(fft_tw, tw, device);
+        fft_scale = scale;
+        fft_ready = true;
+    }
     void ensure_device()
     {
         if (device >= 0) return;
@@ -715,9 +759,14 @@ int ldsp_firfilt_set_mode(ldsp_firfilt_t q, int mode)
 {
     return guard([&] {
         NONNULL(q);
-        LDSP_REQUIRE(mode == LDSP_MODE_FAST || mode == LDSP_MODE_EXACT, "unknown mode");
+        LDSP_REQUIRE(mode == LDSP_MODE_FAST || mode == LDSP_MODE_EXACT || mode == LDSP_MODE_DIRECT, "unknown mode");
         q->mode = mode;
     });
+}
+
+int ldsp_firfilt_get_mode(ldsp_firfilt_t q, int* mode)
+{
+    return guard([&] { NONNULL(q); NONNULL(mode); *mode = q->mode; });
 }
 
 // liquid firfilt_freqresponse: H = scale * sum_i hrev[i] exp(+j 2 pi f i)
@@ -757,7 +806,13 @@ int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int
         if (L > 1 || n > 0) {
             if (q->mode == LDSP_MODE_EXACT)
                 k::fir_exact(q->cplx, dx, hin, hout, n, q->taps_rev.as<float>(), L, q->scale, dy, e.stream);
-            else
+            else if (q->use_fft() && n > 0) {
+                if (!q->fft_ready || q->fft_scale != q->scale) {
+                    LDSP_HIP(hipStreamSynchronize(e.stream));   // tables may be in use by queued work
+                    q->prepare_fft();
+                }
+                k::fir_fft(dx, hin, hout, n, L, q->fft_P(), q->fft_H.p, q->fft_tw.p, dy, e.stream);
+            } else
                 k::fir_fast(q->cplx, dx, hin, hout, n, q->taps_pad.as<float>(), L, q->scale, dy, e.stream);
             if (L > 1) q->cur = 1 - q->cur;
         }

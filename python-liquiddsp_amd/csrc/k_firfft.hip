@@ -1,0 +1,360 @@
+// k_firfft.hip -- overlap-save FFT convolution for the complex FIR filter
+// (firfilt_crcf with real taps: ComplexFIRFilter; the
+// filter semantics are those of firfilt_crcf_execute_block behind
+// src/firfilter.hpp:33 and demod.hpp:135-136).
+//
+// Direct form costs 4 L flop per complex sample (508 at L = 127), which makes
+// it FP32-VALU bound at ~2x the HBM time.  Overlap-save moves it
+// under the HBM roof: every wave owns windows of N points
+//   w = x[b M - P .. b M + M - 1]      (P >= L-1 history samples, M = N - P)
+//   y[b M + i - P] = IFFT(FFT(w) . H)[i]    for i in [P, N)
+// with H = scale * FFT(h zero-padded) / N prepared on the host in float64;
+// ~90 flop per output at L = 127 instead of 508.  Error vs the float64 truth is
+// below the float32 direct form's own (tests/test_gpu_parity.py gates both).
+//
+// Layout: one window per wave, N/64 points per lane, Stockham autosort
+// (N = 512: radices 8, 8, 8; N = 1024: 16, 16, 4).  The first pass works on the
+// coalesced global load (lane l holds w[l + 64 r]); the last pass leaves lane
+// l holding bins l + 64 s, exactly the input layout of the inverse's first
+// pass, so the spectrum multiply needs no exchange.  The inverse is the
+// forward transform of the conjugate.  The two exchanges per transform go
+// through this wave's own padded LDS buffer (bank-conflict free for
+// ds_*_b64) and need no workgroup barrier, so the load / transform / store
+// phases of the 6 resident waves per SIMD overlap freely.  Waves own
+// contiguous runs of windows: the P-sample overlap of consecutive windows is
+// re-read from this CU's L1/L2, not HBM.
+#include "kernels.hpp"
+#include "ldsp_common.hpp"
+
+namespace ldsp {
+namespace k {
+
+namespace {
+
+__device__ __forceinline__ int sl(int i) { return i + (i >> 3); }
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// a * w (complex), fused
+__device__ __forceinline__ float2 cmul(float2 a, float2 w)
+{
+    return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
+}
+// a * (-i)
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
+
+// forward 4-point DFT in place (sign -1)
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3)
+{
+    const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    const float2 t2 = cadd(a1, a3), t3 = mul_mi(csub(a1, a3));
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    a1 = cadd(t1, t3);
+    a3 = csub(t1, t3);
+}
+
+// forward 8-point DFT in place: v[k] = sum_r v[r] exp(-2 pi i r k / 8)
+__device__ __forceinline__ void dft8(float2 (&v)[8])
+{
+    constexpr float r2 = 0.70710678118654752f;
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    dft4(e0, e1, e2, e3);
+    dft4(o0, o1, o2, o3);
+    // W8^1 = (1 - i)/sqrt2, W8^2 = -i, W8^3 = (-1 - i)/sqrt2
+    const float2 w1 = make_float2((o1.x + o1.y) * r2, (o1.y - o1.x) * r2);
+    const float2 w2 = mul_mi(o2);
+    const float2 w3 = make_float2((o3.y - o3.x) * r2, -(o3.x + o3.y) * r2);
+    v[0] = cadd(e0, o0);
+    v[4] = csub(e0, o0);
+    v[1] = cadd(e1, w1);
+    v[5] = csub(e1, w1);
+    v[2] = cadd(e2, w2);
+    v[6] = csub(e2, w2);
+    v[3] = cadd(e3, w3);
+    v[7] = csub(e3, w3);
+}
+
+constexpr int kWN_ = 1024;
+
+__device__ __forceinline__ int wsl(int i) { return i + (i >> 4); }
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ float2 cmulk(float2 a, float wr, float wi)
+{
+    return make_float2(fmaf(a.x, wr, -a.y * wi), fmaf(a.x, wi, a.y * wr));
+}
+
+// forward 16-point DFT (4 x 4): out[k + 4 m]
+__device__ __forceinline__ void dft16(float2 (&v)[16])
+{
+    constexpr float c = 0.92387953251128674f, s = 0.38268343236508977f, r2 = 0.70710678118654752f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) dft4(v[j], v[j + 4], v[j + 8], v[j + 12]);
+    // b[j][k] = v[j + 4 k] *= W16^{jk}
+    v[5] = cmulk(v[5], c, -s);                                   // j1 k1
+    v[9] = make_float2((v[9].x + v[9].y) * r2, (v[9].y - v[9].x) * r2);   // j1 k2: W8
+    v[13] = cmulk(v[13], s, -c);                                 // j1 k3
+    v[6] = make_float2((v[6].x + v[6].y) * r2, (v[6].y - v[6].x) * r2);   // j2 k1: W8
+    v[10] = mul_mi(v[10]);                                       // j2 k2: -i
+    v[14] = make_float2((v[14].y - v[14].x) * r2, -(v[14].x + v[14].y) * r2);   // j2 k3: W16^6
+    v[7] = cmulk(v[7], s, -c);                                   // j3 k1: W16^3
+    v[11] = make_float2((v[11].y - v[11].x) * r2, -(v[11].x + v[11].y) * r2);   // j3 k2: W16^6
+    v[15] = cmulk(v[15], -c, s);                                 // j3 k3: W16^9
+    // DFT4 over j for each k: inputs v[4k + j]... (b[j][k] sits at v[j + 4k])
+#pragma unroll
+    for (int k = 0; k < 4; k++) dft4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    // now v[4k + m] = X[k + 4m]; transpose to v[i] = X[i]
+    float2 o[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int m = 0; m < 4; m++) o[k + 4 * m] = v[4 * k + m];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = o[i];
+}
+
+// forward 1024-point FFT of one wave's window held as v[r] = data[lane + 64 r];
+// on return v[s] = X[lane + 64 s].  d: this wave's padded LDS buffer.
+__device__ __forceinline__ void fft1024(float2 (&v)[16], float2* d, const float2* tw, int lane)
+{
+    dft16(v);
+#pragma unroll
+    for (int r = 0; r < 16; r++) d[wsl(lane * 16 + r)] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 16; r++) v[r] = d[wsl(lane + 64 * r)];
+    const int k = lane & 15;
+#pragma unroll
+    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw[(r - 1) * 16 + k]);
+    dft16(v);
+    wave_lds_sync();
+    const int o = (lane >> 4) * 256 + k;
+#pragma unroll
+    for (int r = 0; r < 16; r++) d[wsl(o + 16 * r)] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int jj = lane + 64 * q;
+        float2 a0 = d[wsl(jj)], a1 = d[wsl(jj + 256)], a2 = d[wsl(jj + 512)], a3 = d[wsl(jj + 768)];
+        a1 = cmul(a1, tw[240 + jj]);
+        a2 = cmul(a2, tw[240 + 256 + jj]);
+        a3 = cmul(a3, tw[240 + 512 + jj]);
+        dft4(a0, a1, a2, a3);
+        v[q] = a0;
+        v[q + 4] = a1;
+        v[q + 8] = a2;
+        v[q + 12] = a3;
+    }
+    wave_lds_sync();
+}
+
+__device__ __forceinline__ void fft512(float2 (&v)[8], float2* d, const float2* tw, int lane)
+{
+    dft8(v);
+#pragma unroll
+    for (int r = 0; r < 8; r++) d[sl(lane * 8 + r)] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = d[sl(lane + 64 * r)];
+    const int k = lane & 7;
+#pragma unroll
+    for (int r = 1; r < 8; r++) v[r] = cmul(v[r], tw[(r - 1) * 8 + k]);
+    dft8(v);
+    wave_lds_sync();
+    const int o = (lane >> 3) * 64 + k;
+#pragma unroll
+    for (int r = 0; r < 8; r++) d[sl(o + 8 * r)] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = d[sl(lane + 64 * r)];
+#pragma unroll
+    for (int r = 1; r < 8; r++) v[r] = cmul(v[r], tw[56 + (r - 1) * 64 + lane]);
+    dft8(v);
+    // v[r] = X[lane + 64 r]
+}
+
+
+template <int PPL>
+__device__ __forceinline__ void load_win(float2 (&v)[PPL], const float2* __restrict__ x,
+                                         const float2* __restrict__ hist, long n, int halo, long g0, int lane)
+{
+    if (g0 >= 0 && g0 + 64 * PPL <= n) {          // interior window: 32-bit lane offsets, no checks
+        const float2* __restrict__ xb = x + g0;
+#pragma unroll
+        for (int r = 0; r < PPL; r++) v[r] = xb[lane + 64 * r];
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < PPL; r++) {
+        const long gi = g0 + lane + 64 * r;
+        float2 e = make_float2(0.0f, 0.0f);
+        if (gi >= 0) {
+            if (gi < n) e = x[gi];
+        } else if (gi >= -halo) {
+            e = hist[gi + halo];
+        }
+        v[r] = e;
+    }
+}
+
+template <int PPL>
+__device__ __forceinline__ void store_win(const float2 (&v)[PPL], float2* __restrict__ y, long n, int P, long g0,
+                                          int lane)
+{
+    // v[s] = conj(y_block[lane + 64 s]);  y[b M + i - P] = y_block[i] for i >= P
+    float2* __restrict__ yb = y + g0;
+    if (g0 + 64 * PPL <= n) {
+#pragma unroll
+        for (int s = 0; s < PPL; s++) {
+            const int i = lane + 64 * s;
+            if (i >= P) yb[i] = make_float2(v[s].x, -v[s].y);
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < PPL; s++) {
+            const int i = lane + 64 * s;
+            if (i >= P && g0 + i < n) yb[i] = make_float2(v[s].x, -v[s].y);
+        }
+    }
+}
+
+__device__ __forceinline__ void write_hist(const float2* __restrict__ x, const float2* __restrict__ hist,
+                                           float2* __restrict__ hist_out, long n, int halo, int t, int nt)
+{
+    for (int j = t; j < halo; j += nt) {
+        const long gi = n - halo + j;
+        hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+    }
+}
+
+// 512-point windows: 8 points per lane, 4 waves per workgroup; tables in LDS.
+constexpr int kVN = 512;
+constexpr int kVSlots = kVN + kVN / 8;
+constexpr int kVWaves = 4;
+
+__global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __restrict__ x,
+                                                             const float2* __restrict__ hist,
+                                                             float2* __restrict__ hist_out, long n, int L, int P,
+                                                             long nwin, long per, const float2* __restrict__ H,
+                                                             const float2* __restrict__ tw, float2* __restrict__ y)
+{
+    __shared__ float2 buf[kVWaves][kVSlots];
+    __shared__ float2 ltw[kFft512Tw];
+    __shared__ float2 lH[kVN];
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int M = kVN - P;
+    const int halo = L - 1;
+    if (blockIdx.x == 0) write_hist(x, hist, hist_out, n, halo, t, 64 * kVWaves);
+    for (int j = t; j < kFft512Tw; j += 64 * kVWaves) ltw[j] = tw[j];
+    for (int j = t; j < kVN; j += 64 * kVWaves) lH[j] = H[j];
+    __syncthreads();
+    const long w0 = ((long)blockIdx.x * kVWaves + wave) * per;
+    const long w1 = min(nwin, w0 + per);
+    float2* d = buf[wave];
+    for (long w = w0; w < w1; w++) {
+        const long g0 = w * M - P;
+        float2 v[8];
+        load_win<8>(v, x, hist, n, halo, g0, lane);
+        fft512(v, d, ltw, lane);
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const float2 p = cmul(v[s], lH[lane + 64 * s]);
+            v[s] = make_float2(p.x, -p.y);
+        }
+        wave_lds_sync();       // pass-3 reads of d are done before pass-1 writes
+        fft512(v, d, ltw, lane);
+        store_win<8>(v, y, n, P, g0, lane);
+        wave_lds_sync();
+    }
+}
+
+// 1024-point windows (P > 128): 16 points per lane, 8 waves per workgroup.
+constexpr int kWSlots = kWN_ + kWN_ / 16;
+constexpr int kWaves = 8;
+
+__global__ void __launch_bounds__(64 * kWaves) k_fir_fft1024(const float2* __restrict__ x,
+                                                             const float2* __restrict__ hist,
+                                                             float2* __restrict__ hist_out, long n, int L, int P,
+                                                             long nwin, long per, const float2* __restrict__ H,
+                                                             const float2* __restrict__ tw, float2* __restrict__ y)
+{
+    __shared__ float2 buf[kWaves][kWSlots];
+    __shared__ float2 ltw[kFft1024Tw];
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int M = kWN_ - P;
+    const int halo = L - 1;
+    if (blockIdx.x == 0) write_hist(x, hist, hist_out, n, halo, t, 64 * kWaves);
+    for (int j = t; j < kFft1024Tw; j += 64 * kWaves) ltw[j] = tw[j];
+    __syncthreads();
+    const long w0 = ((long)blockIdx.x * kWaves + wave) * per;
+    const long w1 = min(nwin, w0 + per);
+    float2* d = buf[wave];
+    for (long w = w0; w < w1; w++) {
+        asm volatile("" ::: "memory");    // keep H reads inside the loop (register budget)
+        const long g0 = w * M - P;
+        float2 v[16];
+        load_win<16>(v, x, hist, n, halo, g0, lane);
+        fft1024(v, d, ltw, lane);
+#pragma unroll
+        for (int s = 0; s < 16; s++) {
+            const float2 p = cmul(v[s], H[lane + 64 * s]);
+            v[s] = make_float2(p.x, -p.y);
+        }
+        fft1024(v, d, ltw, lane);
+        store_win<16>(v, y, n, P, g0, lane);
+    }
+}
+
+// Waves resident on the device for a kernel (CUs x blocks per CU x waves per block).
+long resident_waves(const void* fn, int threads)
+{
+    int dev = 0, cus = 0, per_cu = 0;
+    LDSP_HIP(hipGetDevice(&dev));
+    LDSP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    LDSP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0));
+    return (long)std::max(1, cus) * std::max(1, per_cu) * (threads / 64);
+}
+
+} // namespace
+
+int fir_fft_points(int P) { return P <= 128 ? kVN : kWN_; }
+
+void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, int P, const void* H, const void* tw,
+             void* y, hipStream_t s)
+{
+    if (n == 0) return;
+    const bool small = P <= 128;
+    const long N = small ? kVN : kWN_;
+    const long M = N - P;
+    const long nwin = (long)((n + M - 1) / M);
+    static long slots512 = 0, slots1024 = 0;
+    long& slots = small ? slots512 : slots1024;
+    if (slots == 0)
+        slots = small ? resident_waves((const void*)k_fir_fft512, 64 * kVWaves)
+                      : resident_waves((const void*)k_fir_fft1024, 64 * kWaves);
+    const int wpb = small ? kVWaves : kWaves;
+    const long waves = std::min(nwin, slots);
+    const long per = (nwin + waves - 1) / waves;       // contiguous windows per wave
+    const long used = (nwin + per - 1) / per;
+    const unsigned grid = (unsigned)((used + wpb - 1) / wpb);
+    LDSP_PROF(s, "k_fir_fft");
+    if (small)
+        hipLaunchKernelGGL(k_fir_fft512, dim3(grid), dim3(64 * kVWaves), 0, s, (const float2*)x,
+                           (const float2*)hist, (float2*)hist_out, (long)n, L, P, nwin, per, (const float2*)H,
+                           (const float2*)tw, (float2*)y);
+    else
+        hipLaunchKernelGGL(k_fir_fft1024, dim3(grid), dim3(64 * kWaves), 0, s, (const float2*)x,
+                           (const float2*)hist, (float2*)hist_out, (long)n, L, P, nwin, per, (const float2*)H,
+                           (const float2*)tw, (float2*)y);
+    LDSP_HIP(hipGetLastError());
+}
+
+} // namespace k
+} // namespace ldsp

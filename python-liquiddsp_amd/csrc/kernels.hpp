@@ -20,6 +20,19 @@ void fir_exact(bool cplx, const void* x, const void* hist, void* hist_out, size_
                const float* taps_rev, int L, float scale, void* y, hipStream_t s);
 // history update only (n == 0 calls skip the kernels)
 
+// Overlap-save FFT convolution (complex samples, real taps), k_firfft.hip.
+// P = history samples per window (L - 1 <= P <= 512, multiple of 64); the
+// window has fir_fft_points(P) = 512 (P <= 128) or 1024 points.
+// H[N] = scale * FFT(h) / N for that N; tw = Stockham twiddles
+// exp(-2 pi i r k / (Ns R)) laid out [pass][r-1][k]:
+//   N = 512 : (Ns, R) = (8, 8), (64, 8)      -> kFft512Tw entries
+//   N = 1024: (Ns, R) = (16, 16), (256, 4)   -> kFft1024Tw entries
+constexpr int kFft512Tw = 7 * 8 + 7 * 64;
+constexpr int kFft1024Tw = 15 * 16 + 3 * 256;
+int fir_fft_points(int P);
+void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, int P, const void* H, const void* tw,
+             void* y, hipStream_t s);
+
 // ------------------------------------------------------------------ resampler
 struct ResampPlan {
     uint64_t P0;          // phase at call start (resamp "phase", < 2^24 + step)

@@ -171,6 +171,24 @@ struct FIR {
         check(ldsp_firfilt_set_mode(q, e ? LDSP_MODE_EXACT : LDSP_MODE_FAST));
         exact_ = e;
     }
+    // "fast" (default: overlap-save FFT for complex data and 48..1025 taps),
+    // "direct" (register-blocked direct form), "exact" (liquid order, bitwise)
+    std::string get_mode()
+    {
+        int m;
+        check(ldsp_firfilt_get_mode(q, &m));
+        return m == LDSP_MODE_EXACT ? "exact" : (m == LDSP_MODE_DIRECT ? "direct" : "fast");
+    }
+    void set_mode(const std::string& m)
+    {
+        int v;
+        if (m == "fast") v = LDSP_MODE_FAST;
+        else if (m == "direct") v = LDSP_MODE_DIRECT;
+        else if (m == "exact") v = LDSP_MODE_EXACT;
+        else throw py::value_error("mode must be 'fast', 'direct' or 'exact'");
+        check(ldsp_firfilt_set_mode(q, v));
+        exact_ = v == LDSP_MODE_EXACT;
+    }
     py::array_t<float> taps()
     {
         unsigned n;
@@ -822,6 +840,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("__call__", &RealFIRFilter::call)
         .def("reset", &RealFIRFilter::reset)
         .def_property("exact", &RealFIRFilter::get_exact, &RealFIRFilter::set_exact)
+        .def_property("mode", &RealFIRFilter::get_mode, &RealFIRFilter::set_mode)
         .def_property_readonly("taps", &RealFIRFilter::taps);
     py::class_<ComplexFIRFilter>(m, "ComplexFIRFilter")
         .def(py::init<py::handle>(), py::arg("h"))
@@ -829,6 +848,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("__call__", &ComplexFIRFilter::call)
         .def("reset", &ComplexFIRFilter::reset)
         .def_property("exact", &ComplexFIRFilter::get_exact, &ComplexFIRFilter::set_exact)
+        .def_property("mode", &ComplexFIRFilter::get_mode, &ComplexFIRFilter::set_mode)
         .def_property_readonly("taps", &ComplexFIRFilter::taps);
     py::class_<RealDCBlocker>(m, "RealDCBlocker")
         .def(py::init<int, float>(), py::arg("slen") = 25, py::arg("As") = 20.0f)
@@ -836,6 +856,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("__call__", &RealDCBlocker::call)
         .def("reset", &RealDCBlocker::reset)
         .def_property("exact", &RealDCBlocker::get_exact, &RealDCBlocker::set_exact)
+        .def_property("mode", &RealDCBlocker::get_mode, &RealDCBlocker::set_mode)
         .def_property_readonly("taps", &RealDCBlocker::taps);
     py::class_<RealKaiserBessel>(m, "RealKaiserBessel")
         .def(py::init<int, float, float, float>(), py::arg("flen") = 25, py::arg("Fc"), py::arg("As") = 20.0f,
@@ -844,6 +865,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("__call__", &RealKaiserBessel::call)
         .def("reset", &RealKaiserBessel::reset)
         .def_property("exact", &RealKaiserBessel::get_exact, &RealKaiserBessel::set_exact)
+        .def_property("mode", &RealKaiserBessel::get_mode, &RealKaiserBessel::set_mode)
         .def_property_readonly("taps", &RealKaiserBessel::taps)
         .def_property_readonly("scale", &RealKaiserBessel::get_scale);
 }

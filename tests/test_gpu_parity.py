@@ -71,11 +71,14 @@ def test_device_math_bitwise(ld, ora, rng):
 # ------------------------------------------------------------------ FIR
 @pytest.mark.parametrize("L", L_TAPS)
 @pytest.mark.parametrize("cplx", [True, False])
-def test_fir_fast_within_1e6(ld, ora, rng, L, cplx):
+@pytest.mark.parametrize("mode", ["fast", "direct"])
+def test_fir_fast_within_1e6(ld, ora, rng, L, cplx, mode):
+    # complex "fast" with 48 <= L <= 1025 is the overlap-save FFT kernel
     h = ora.firdes_kaiser(L, 0.1, 60.0) if L > 1 else np.float32([0.7])
     n = 70_001
     x = cgauss(rng, n) if cplx else np.float32(rng.standard_normal(n))
     g = (ld.ComplexFIRFilter if cplx else ld.RealFIRFilter)(h)
+    g.mode = mode
     o = ora.FIRFilter(h, cplx=cplx)
     # ragged streaming: history carried across calls
     cuts = [0, 1, 5, 4096, 4097, 30_000, n]
@@ -105,16 +108,50 @@ def test_fir_exact_bitwise(ld, ora, rng, L, cplx):
     assert_bitwise(y, o(x))
 
 
-def test_fir_fast_chunking_invariant(ld, ora, rng):
+@pytest.mark.parametrize("mode", ["fast", "direct"])
+def test_fir_fast_chunking_invariant(ld, ora, rng, mode):
+    # direct form: bitwise invariant to how the stream is cut into calls;
+    # overlap-save FFT: the 2048-point windows move with the call boundaries,
+    # so a re-cut stream agrees to float32 rounding (<= 1e-6 of max|y|)
     h = ora.firdes_kaiser(127, 0.1, 60.0)
     x = cgauss(rng, 50_000)
     a = ld.ComplexFIRFilter(h)
+    a.mode = mode
     whole = a(x)
     b = ld.ComplexFIRFilter(h)
+    b.mode = mode
     parts = np.concatenate([b(x[:7]), b(x[7:4100]), b(x[4100:])])
-    assert_bitwise(parts, whole)
+    if mode == "direct":
+        assert_bitwise(parts, whole)
+    else:
+        assert maxrel(parts, whole) <= 1e-6
     a.reset()
     assert_bitwise(a(x), whole)
+
+
+@pytest.mark.parametrize("L", [127, 255])
+def test_fir_fft_north_star_size(ld, ora, rng, L):
+    """BASELINE north-star size (64 Mi complex64): the FFT path against the
+    direct-form kernel over the whole array (size-independent property: both
+    within float32 rounding of the same convolution) and against the
+    restatement on a 256 Ki-sample window taken from the middle."""
+    import torch
+    n = 64 << 20
+    h = ora.firdes_kaiser(L, 0.1, 60.0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    xd = torch.complex(torch.randn(n, generator=g, device="cuda"), torch.randn(n, generator=g, device="cuda"))
+    f = ld.ComplexFIRFilter(h)
+    d = ld.ComplexFIRFilter(h)
+    d.mode = "direct"
+    yf = f(xd)
+    yd = d(xd)
+    err = float((yf - yd).abs().max() / yd.abs().max())
+    assert err <= 1e-6, err
+    s0, w = n // 2 + 12345, 1 << 18
+    xw = xd[s0 - (L - 1): s0 + w].cpu().numpy()
+    ref = ora.FIRFilter(h, cplx=True)(xw)[L - 1:]
+    assert maxrel(yf[s0: s0 + w].cpu().numpy(), ref) <= 1e-6
 
 
 def test_kaiserbessel_dcblocker(ld, ora, rng):
