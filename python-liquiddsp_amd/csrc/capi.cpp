@@ -269,6 +269,8 @@ struct IirObj {
     int spec_W = 0;                   // > 0: fast-decaying filter -> speculative exact chunks
     int device = -1;
     DevBuf db, da, st32, st64, sc1, sc2, mats;
+    DevBuf bmats, bsc1, bsc2, bsc3;   // blocked scan (D <= 8): matrices and scratch
+    int bplan_G = 0;
     bool state_in64 = false;          // where the authoritative state lives
     int plan_C = 0;
     long plan_nch = 0;
@@ -414,6 +416,43 @@ struct IirObj {
             LDSP_HIP(hipMemcpy(st32.p, f.data(), f.size() * 4, hipMemcpyHostToDevice));
         }
         state_in64 = to64;
+    }
+    // Blocked scan plan (k_iir_blk): 256-sample chunks, 256 chunks per block.
+    k::IirBlkPlan blk_plan(size_t n)
+    {
+        const long C = k::kIirBlkChunk, CB = C * k::kIirBlkChunks;
+        const long nch = (long)((n + C - 1) / C);
+        const long nblk = (long)((n + CB - 1) / CB);
+        const int G = (int)((nblk + 1023) / 1024);
+        const size_t DD = (size_t)D * D;
+        if (G != bplan_G) {
+            std::vector<double> all;
+            std::vector<double> M = matpow(A, (uint64_t)C);
+            for (int l = 0; l < 8; l++) {                     // A^{C 2^l}
+                all.insert(all.end(), M.begin(), M.end());
+                M = matmul(M, M);
+            }
+            const std::vector<double> AB = matpow(A, (uint64_t)CB);
+            all.insert(all.end(), AB.begin(), AB.end());
+            M = matpow(AB, (uint64_t)G);
+            for (int l = 0; l < 10; l++) {                    // A^{CB G 2^l}
+                all.insert(all.end(), M.begin(), M.end());
+                M = matmul(M, M);
+            }
+            upload(bmats, all, device);
+            bplan_G = G;
+        }
+        k::IirBlkPlan p;
+        p.nchunks = nch;
+        p.nblk = nblk;
+        p.G = G;
+        p.AL = bmats.as<double>();
+        p.AB = p.AL + 8 * DD;
+        p.AG = p.AB + DD;
+        p.local = (double*)bsc1.ensure((size_t)nch * ncomp() * D * sizeof(double), device);
+        p.blocal = (double*)bsc2.ensure((size_t)nblk * ncomp() * D * sizeof(double), device);
+        p.bstart = (double*)bsc3.ensure((size_t)nblk * ncomp() * D * sizeof(double), device);
+        return p;
     }
     k::IirScanPlan scan_plan(size_t n)
     {
@@ -1198,6 +1237,10 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
             } else if (q->mode == LDSP_MODE_EXACT) {
                 q->state_to(false, e.stream);
                 k::iir_seq(q->cplx, d, dx, n, q->st32.as<float>(), dy, e.stream);
+            } else if (q->D <= k::kIirBlkMaxD && !std::getenv("LDSP_IIR_OLDSCAN")) {
+                q->state_to(true, e.stream);
+                const k::IirBlkPlan p = q->blk_plan(n);
+                k::iir_blk(q->cplx, d, q->b.data(), q->a.data(), dx, n, q->st64.as<double>(), p, dy, e.stream);
             } else {
                 q->state_to(true, e.stream);
                 const k::IirScanPlan p = q->scan_plan(n);

@@ -16,6 +16,8 @@
 //             bit-for-bit with the true one; a single-wave verifier compares
 //             every chunk's guessed start state with its predecessor's end state
 //             and re-runs the (rare) chunks that did not coalesce.
+#include <type_traits>
+
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 
@@ -483,6 +485,307 @@ void launch_carry(int ncomp, const IirScanPlan& p, const double* state64, hipStr
     LDSP_HIP(hipGetLastError());
 }
 
+// --------------------------------------------------------------- blocked float64 scan
+// Replaces K1/K3 above for state dimension D <= 8 (SOS up to 4 sections, TF up
+// to 9 taps).  Chunks of kBC samples, kBN chunks per block (one workgroup,
+// one chunk per thread):
+//   k_iir_blk<FINAL=false>: every chunk from a zero state -> local end state
+//       L_j (global); in-block Hillis-Steele scan E_j = L_j + A^C E_{j-1}
+//       -> block local end state BL_b.
+//   k_iir_scan_carry over blocks (A^{kBC kBN}) -> block start states BS_b.
+//   k_iir_blk<FINAL=true>: the same in-block scan with E_0 += A^C BS_b gives
+//       every chunk's true start state; chunks re-run writing outputs.
+// Input and output tiles (kBT samples x 64 chunks per wave) are staged through
+// LDS so that every global access is coalesced; both components of a complex
+// stream run in the same lane (two independent dependence chains).  Per
+// section the recurrence is arranged so that only v0 = t - (a1 v1 + a2 v2)
+// and t' = b0 v0 + (b1 v1 + b2 v2) sit on the sample-to-sample critical path.
+constexpr int kBC = 256;   // samples per chunk
+constexpr int kBT = 16;    // samples per staged tile
+constexpr int kBN = 256;   // chunks per block = threads per workgroup
+
+template <int D>
+struct StepSos {           // D = 2 nsos; state (v[2s], v[2s+1]) = (v1, v2) of section s
+    double b[D / 2][3], a[D / 2][3];
+    __device__ __forceinline__ double operator()(double (&v)[D], double x) const
+    {
+        double t = x;
+#pragma unroll
+        for (int s = 0; s < D / 2; s++) {
+            const double v1 = v[2 * s], v2 = v[2 * s + 1];
+            const double pa = fma(a[s][2], v2, a[s][1] * v1);
+            const double pb = fma(b[s][2], v2, b[s][1] * v1);
+            const double v0 = t - pa;
+            t = fma(b[s][0], v0, pb);
+            v[2 * s + 1] = v1;
+            v[2 * s] = v0;
+        }
+        return t;
+    }
+};
+
+template <int D>
+struct StepTf {            // nv = D + 1 taps; v[i] = w[n - 1 - i]
+    double b[D + 1], a[D + 1];
+    __device__ __forceinline__ double operator()(double (&v)[D], double x) const
+    {
+        double pa = 0.0, pb = 0.0;
+#pragma unroll
+        for (int i = D; i >= 1; i--) {
+            pa = fma(a[i], v[i - 1], pa);
+            pb = fma(b[i], v[i - 1], pb);
+        }
+        const double r = x - pa;
+#pragma unroll
+        for (int i = D - 1; i > 0; i--) v[i] = v[i - 1];
+        v[0] = r;
+        return fma(b[0], r, pb);
+    }
+};
+
+template <int NC>
+struct SampT {
+    using T = float2;
+    static __device__ __forceinline__ double get(const float2& s, int c) { return c ? (double)s.y : (double)s.x; }
+    static __device__ __forceinline__ void put(float2& s, int c, float v) { if (c) s.y = v; else s.x = v; }
+};
+template <>
+struct SampT<1> {
+    using T = float;
+    static __device__ __forceinline__ double get(const float& s, int) { return (double)s; }
+    static __device__ __forceinline__ void put(float& s, int, float v) { s = v; }
+};
+
+__device__ __forceinline__ void iir_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// D x D matvec out += M in (M row-major in global memory, uniform across lanes)
+template <int D>
+__device__ __forceinline__ void mv_acc(const double* __restrict__ M, const double (&in)[D], double (&out)[D])
+{
+#pragma unroll
+    for (int r = 0; r < D; r++) {
+        double acc = out[r];
+#pragma unroll
+        for (int q = 0; q < D; q++) acc = fma(M[r * D + q], in[q], acc);
+        out[r] = acc;
+    }
+}
+
+template <int NC, int D, bool FINAL, class Step>
+__global__ void __launch_bounds__(kBN) k_iir_blk(Step step, const float* __restrict__ xf, long n, long nch,
+                                                 const double* __restrict__ AL, double* __restrict__ Lloc,
+                                                 const double* __restrict__ BS, double* __restrict__ BL,
+                                                 double* __restrict__ state64, float* __restrict__ yf)
+{
+    using S = SampT<NC>;
+    using T = typename S::T;
+    constexpr int kRow = kBT + 1;
+    __shared__ T stage[kBN / 64][64 * kRow];
+    __shared__ double scn[kBN][NC][D];
+    const T* __restrict__ x = (const T*)xf;
+    T* __restrict__ y = (T*)yf;
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    const long b = blockIdx.x;
+    const long gc = b * kBN + t;
+    const long wbase = (b * kBN + wave * 64) * (long)kBC;   // first sample of this wave's 64 chunks
+    const long cbase = gc * (long)kBC;                       // first sample of this lane's chunk
+    T* st = stage[wave];
+    double v[NC][D];
+    double E[NC][D];
+
+    // Runs this lane's chunk over the staged tiles from state v.
+    auto run = [&](auto write_tag) {
+        constexpr bool WRITE = decltype(write_tag)::value;
+        T nxt[kBT];
+        auto fetch = [&](int k) {
+#pragma unroll
+            for (int q = 0; q < kBT; q++) {
+                const int e = lane + 64 * q;
+                const long gi = wbase + (long)(e >> 4) * kBC + k * kBT + (e & 15);
+                T z{};
+                nxt[q] = gi < n ? x[gi] : z;
+            }
+        };
+        fetch(0);
+        for (int k = 0; k < kBC / kBT; k++) {
+#pragma unroll
+            for (int q = 0; q < kBT; q++) {
+                const int e = lane + 64 * q;
+                st[(e >> 4) * kRow + (e & 15)] = nxt[q];
+            }
+            if (k + 1 < kBC / kBT) fetch(k + 1);
+            iir_wave_sync();
+            T in[kBT];
+#pragma unroll
+            for (int i = 0; i < kBT; i++) in[i] = st[lane * kRow + i];
+            iir_wave_sync();
+            const long rem = n - (cbase + k * kBT);          // samples of this tile inside the call
+            if (rem >= kBT) {
+#pragma unroll
+                for (int i = 0; i < kBT; i++) {
+                    T o{};
+#pragma unroll
+                    for (int c = 0; c < NC; c++) {
+                        const double r = step(v[c], S::get(in[i], c));
+                        if (WRITE) S::put(o, c, (float)r);
+                    }
+                    if (WRITE) st[lane * kRow + i] = o;
+                }
+            } else {                                          // the call ends inside this tile: stop the state there
+#pragma unroll
+                for (int i = 0; i < kBT; i++) {
+                    T o{};
+                    if (i < rem) {
+#pragma unroll
+                        for (int c = 0; c < NC; c++) {
+                            const double r = step(v[c], S::get(in[i], c));
+                            if (WRITE) S::put(o, c, (float)r);
+                        }
+                    }
+                    if (WRITE) st[lane * kRow + i] = o;
+                }
+            }
+            if (WRITE) {
+                iir_wave_sync();
+#pragma unroll
+                for (int q = 0; q < kBT; q++) {
+                    const int e = lane + 64 * q;
+                    const long gi = wbase + (long)(e >> 4) * kBC + k * kBT + (e & 15);
+                    if (gi < n) y[gi] = st[(e >> 4) * kRow + (e & 15)];
+                }
+                iir_wave_sync();
+            }
+        }
+    };
+
+    if (!FINAL) {
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i < D; i++) v[c][i] = 0.0;
+        run(std::false_type{});
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i < D; i++) {
+                E[c][i] = v[c][i];
+                if (gc < nch) Lloc[(gc * NC + c) * D + i] = v[c][i];
+            }
+    } else {
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i < D; i++) E[c][i] = gc < nch ? Lloc[(gc * NC + c) * D + i] : 0.0;
+        if (t == 0) {
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                double s0[D];
+#pragma unroll
+                for (int i = 0; i < D; i++) s0[i] = BS[(b * NC + c) * D + i];
+                mv_acc<D>(AL, s0, E[c]);
+            }
+        }
+    }
+    // inclusive scan over the block's chunks: E_j = L_j + A^C E_{j-1}
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+#pragma unroll
+        for (int i = 0; i < D; i++) scn[t][c][i] = E[c][i];
+    __syncthreads();
+#pragma unroll 1
+    for (int l = 0; (1 << l) < kBN; l++) {
+        const int dd = 1 << l;
+        if (t >= dd) {
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                double o[D];
+#pragma unroll
+                for (int i = 0; i < D; i++) o[i] = scn[t - dd][c][i];
+                mv_acc<D>(AL + (size_t)l * D * D, o, E[c]);
+            }
+        }
+        __syncthreads();
+        if (t >= dd)
+#pragma unroll
+            for (int c = 0; c < NC; c++)
+#pragma unroll
+                for (int i = 0; i < D; i++) scn[t][c][i] = E[c][i];
+        __syncthreads();
+    }
+    if (!FINAL) {
+        if (t == kBN - 1)
+#pragma unroll
+            for (int c = 0; c < NC; c++)
+#pragma unroll
+                for (int i = 0; i < D; i++) BL[(b * NC + c) * D + i] = E[c][i];
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+#pragma unroll
+        for (int i = 0; i < D; i++) v[c][i] = t == 0 ? BS[(b * NC + c) * D + i] : scn[t - 1][c][i];
+    run(std::true_type{});
+    if (gc == nch - 1)
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i < D; i++) state64[c * D + i] = v[c][i];
+}
+
+template <int NC, int D, class Step>
+void launch_blk(const Step& st, const IirDesc& d, const float* x, size_t n, double* state64, const IirBlkPlan& p,
+                float* y, hipStream_t s)
+{
+    const unsigned g = (unsigned)p.nblk;
+    {
+        LDSP_PROF(s, "k_iir_blk_local");
+        hipLaunchKernelGGL((k_iir_blk<NC, D, false, Step>), dim3(g), dim3(kBN), 0, s, st, x, (long)n, p.nchunks,
+                           p.AL, p.local, (const double*)nullptr, p.blocal, (double*)nullptr, (float*)nullptr);
+    }
+    LDSP_HIP(hipGetLastError());
+    IirScanPlan cp;
+    cp.nchunks = p.nblk;
+    cp.G = p.G;
+    cp.levels = 10;
+    cp.AC = p.AB;
+    cp.AG = p.AG;
+    cp.local = p.blocal;
+    cp.carry = p.bstart;
+    launch_carry<D>(NC, cp, state64, s);
+    {
+        LDSP_PROF(s, "k_iir_blk_final");
+        hipLaunchKernelGGL((k_iir_blk<NC, D, true, Step>), dim3(g), dim3(kBN), 0, s, st, x, (long)n, p.nchunks,
+                           p.AL, p.local, (const double*)p.bstart, (double*)nullptr, state64, y);
+    }
+    LDSP_HIP(hipGetLastError());
+}
+
+template <int NC, int D>
+void dispatch_blk(const IirDesc& d, const float* cb, const float* ca, const float* x, size_t n, double* state64,
+                  const IirBlkPlan& p, float* y, hipStream_t s)
+{
+    if (d.sos) {
+        if constexpr (D % 2 == 0) {
+            StepSos<D> st;
+            for (int q = 0; q < D / 2; q++)
+                for (int k = 0; k < 3; k++) {
+                    st.b[q][k] = (double)cb[3 * q + k];
+                    st.a[q][k] = (double)ca[3 * q + k];
+                }
+            launch_blk<NC, D>(st, d, x, n, state64, p, y, s);
+        }
+    } else {
+        StepTf<D> st;
+        for (int i = 0; i <= D; i++) {
+            st.b[i] = i < d.nb ? (double)cb[i] : 0.0;
+            st.a[i] = i < d.na ? (double)ca[i] : 0.0;
+        }
+        launch_blk<NC, D>(st, d, x, n, state64, p, y, s);
+    }
+}
+
 } // namespace
 
 void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s)
@@ -554,5 +857,28 @@ void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* stat
     LDSP_HIP(hipGetLastError());
 }
 
+} // namespace k
+} // namespace ldsp
+
+namespace ldsp {
+namespace k {
+void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n, double* state64,
+             const IirBlkPlan& p, void* y, hipStream_t s)
+{
+    if (n == 0) return;
+    LDSP_REQUIRE(d.D >= 1 && d.D <= kIirBlkMaxD, "iir: state dimension too large for the blocked scan");
+    const float* xf = (const float*)x;
+    float* yf = (float*)y;
+#define LDSP_BLK(DD)                                                                          \
+    case DD:                                                                                  \
+        if (cplx) dispatch_blk<2, DD>(d, hb, ha, xf, n, state64, p, yf, s);                    \
+        else dispatch_blk<1, DD>(d, hb, ha, xf, n, state64, p, yf, s);                         \
+        break;
+    switch (d.D) {
+        LDSP_BLK(1) LDSP_BLK(2) LDSP_BLK(3) LDSP_BLK(4) LDSP_BLK(5) LDSP_BLK(6) LDSP_BLK(7) LDSP_BLK(8)
+    default: throw Error(LDSP_EUNSUP, "iir: unsupported state dimension");
+    }
+#undef LDSP_BLK
+}
 } // namespace k
 } // namespace ldsp

@@ -82,6 +82,24 @@ struct IirScanPlan {
 };
 void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* state64, const IirScanPlan& p,
               void* y, hipStream_t s);
+// Blocked float64 scan for state dimension D <= kIirBlkMaxD (k_iir_blk):
+// chunks of 256 samples, 256 chunks per block.  hb/ha: host copies of the
+// float32 coefficients (SOS [nsos][3] or TF [nb] / [na]), passed by value.
+constexpr int kIirBlkMaxD = 8;
+constexpr int kIirBlkChunk = 256;
+constexpr int kIirBlkChunks = 256;
+struct IirBlkPlan {
+    long nchunks, nblk;
+    int G;                // blocks per carry thread
+    const double* AL;     // A^{256 * 2^l}, l = 0..7             [8][D*D]
+    const double* AB;     // A^{65536}                            [D*D]
+    const double* AG;     // A^{65536 * G * 2^l}, l = 0..9         [10][D*D]
+    double* local;        // [nchunks][ncomp][D]
+    double* blocal;       // [nblk][ncomp][D]
+    double* bstart;       // [nblk][ncomp][D]
+};
+void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n, double* state64,
+             const IirBlkPlan& p, void* y, hipStream_t s);
 // Speculative exact evaluation for fast-decaying filters: chunks start from a
 // zero state W samples early; a verifier re-runs any chunk whose guessed
 // start state differs bit-wise from its predecessor's end state.

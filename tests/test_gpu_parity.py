@@ -256,7 +256,7 @@ def test_iir_exact_bitwise(ld, ora, rng):
     assert_bitwise(y, o(x))
 
 
-@pytest.mark.parametrize("n", [5000, 1 << 20])
+@pytest.mark.parametrize("n", [5000, 3 * 65536 + 17, 1 << 20, 1 << 26])
 def test_iir_fast_scan_accuracy(ld, ora, rng, n):
     x = cgauss(rng, n)
     g = ld.ComplexIIRFilter(**CHAIN_IIR)
@@ -280,6 +280,25 @@ def test_iir_real_variants(ld, ora, rng):
     g2 = ld.RLowpassIIR("cheby1", 5, 0.2)
     o2 = ora.IIRFilter(prototype=("cheby1", "lowpass", 1, 5, 0.2, 0.1, 0.5, 20.0), cplx=False)
     assert maxrel(g2(x), o2.execute_f64(x)) < 1e-6
+
+
+@pytest.mark.parametrize("cplx", [False, True])
+def test_iir_blocked_scan_multiblock(ld, ora, rng, cplx):
+    """Blocked float64 scan (k_iir_blk, D <= 8) across several 65 536-sample
+    blocks and ragged call boundaries, SOS and raw transfer-function forms,
+    against the float64 sequential evaluation."""
+    n = 5 * 65536 + 333
+    x = cgauss(rng, n) if cplx else np.float32(rng.standard_normal(n))
+    cuts = [0, 1000, 65536 + 7, 4 * 65536, n]
+    g = (ld.ComplexIIRFilter if cplx else ld.RealIIRFilter)(filter_type="cheby2", order=8, Fc=0.02)
+    o = ora.IIRFilter(prototype=("cheby2", "lowpass", 1, 8, np.float32(0.02), 0.3, 0.7, 60.0), cplx=cplx)
+    y = np.concatenate([g(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert maxrel(y, o.execute_f64(x)) <= 1e-6
+    b_, a_ = sps.butter(2, 0.002)             # slow decay (not the speculative-exact path), stable in float32
+    gt = (ld.CIIRFilter if cplx else ld.RIIRFilter)(np.float32(b_), np.float32(a_))
+    ot = ora.IIRFilter(tf=(np.float32(b_), np.float32(a_)), cplx=cplx)
+    yt = np.concatenate([gt(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert maxrel(yt, ot.execute_f64(x)) <= 1e-6
 
 
 def test_tf_iir_and_deemphasis_bitwise(ld, ora, rng):
