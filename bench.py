@@ -187,6 +187,7 @@ def main():
     # attribute the stage minimum to the kernel that produces the stage output.
     n = args.n
     alg = {"k_iir_scan_local": 8 * n, "k_iir_scan_carry": 0, "k_iir_scan_final": 16 * n,
+           "k_iir_blk_local": 8 * n, "k_iir_blk_final": 16 * n,
            "k_resamp": 8 * n + 8 * n_pcm, "k_agc_chunks": 16 * n_pcm, "k_agc_verify": 0,
            "k_fir_exact": 8 * n_pcm + 8 * n_pcm, "k_pll_cand": 12 * n_pcm, "k_pll_walk": 12 * n_pcm,
            "k_iir_spec_chunks": 8 * n_pcm, "k_iir_spec_verify": 0, "k_delay_hist": 0}
@@ -218,7 +219,8 @@ def main():
                    "pcm_samples_per_step": n_pcm, "parallelism": f"channel-per-gpu x{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "ms_per_launch": round(dom_ms, 4),
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("bench", dom),
+                     "traffic_source": PMC_SOURCE,
                      "note": "alg bytes = 12 B per PCM sample (AmpModem in + out); the PLL recurrence is "
                              "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else ""},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
@@ -232,6 +234,29 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def _pmc_summary():
+    """Latest committed rocprofv3 PMC summary (scripts/prof_round.sh ->
+    profiles/rNN_pmc_summary.json): per-kernel HBM bytes per launch from
+    FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, measured on the same
+    commands in separate --pmc passes."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], REPO)
+
+
+PMC, PMC_SOURCE = _pmc_summary()
+
+
+def pmc_traffic(run, kernel):
+    try:
+        return round(PMC[run][kernel]["hbm_bytes"])
+    except (TypeError, KeyError):
+        return None
 
 
 def components(L, device, reps=5):
@@ -269,6 +294,12 @@ def components(L, device, reps=5):
         out[f"fir127_64Mi_{mode}"] = {"kernel": kn, "ms": round(ms, 4), "GBs": round(16 * n / ms / 1e6, 1),
                                       "hbm_frac": round(16 * n / ms / 1e6 / HBM_PEAK_GBS, 4),
                                       "direct_form_TFLOPs": round(4 * 127 * n / ms / 1e9, 2)}
+        if mode == "fast":      # north-star roofline line: 16 B per complex sample (read + write once)
+            out["north_star_roofline"] = {
+                "kernel": "k_fir_fft512", "bound": "hbm", "achieved": round(16 * n / ms / 1e6, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(16 * n / ms / 1e6 / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic("fir", "k_fir_fft512"), "traffic_source": PMC_SOURCE,
+                "alg_bytes": 16 * n, "target_frac": 0.5}
     del xs
     n = 256 << 20
     xs = torch.complex(torch.randn(n, generator=g, device=device), torch.randn(n, generator=g, device=device))

@@ -344,7 +344,7 @@ void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, i
     const long per = (nwin + waves - 1) / waves;       // contiguous windows per wave
     const long used = (nwin + per - 1) / per;
     const unsigned grid = (unsigned)((used + wpb - 1) / wpb);
-    LDSP_PROF(s, "k_fir_fft");
+    LDSP_PROF(s, small ? "k_fir_fft512" : "k_fir_fft1024");
     if (small)
         hipLaunchKernelGGL(k_fir_fft512, dim3(grid), dim3(64 * kVWaves), 0, s, (const float2*)x,
                            (const float2*)hist, (float2*)hist_out, (long)n, L, P, nwin, per, (const float2*)H,

@@ -1,0 +1,64 @@
+"""Per-kernel summary of a prof_round.sh directory: average duration (kernel
+trace) and HBM bytes per launch from FETCH_SIZE / WRITE_SIZE.
+
+gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE (KB) reports half the
+bytes of a wide coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024;
+WRITE_SIZE (KB) is exact for streaming stores: write bytes = WRITE_SIZE * 1024.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"(k_\w+)(<[^>]*>)?", name)
+    if not m:
+        return name[:60]
+    if m.group(1) == "k_iir_blk" and m.group(2):      # k_iir_blk<NC, D, FINAL, ...>
+        return "k_iir_blk_final" if "true" in m.group(2) else "k_iir_blk_local"
+    return m.group(1)
+
+
+def stats(d):
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            out[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+    return out
+
+
+def counters(d, counter):
+    acc = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main(root):
+    res = {}
+    for run in ("bench", "fir"):
+        st = stats(os.path.join(root, f"{run}_trace"))
+        fe = counters(os.path.join(root, f"{run}_fetch"), "FETCH_SIZE")
+        wr = counters(os.path.join(root, f"{run}_write"), "WRITE_SIZE")
+        for k, v in st.items():
+            e = dict(v)
+            if k in fe:
+                e["fetch_bytes_corrected"] = 2.0 * fe[k] * 1024
+            if k in wr:
+                e["write_bytes"] = wr[k] * 1024
+            if "fetch_bytes_corrected" in e and "write_bytes" in e:
+                e["hbm_bytes"] = e["fetch_bytes_corrected"] + e["write_bytes"]
+                e["hbm_GBs"] = round(e["hbm_bytes"] / (e["avg_us"] * 1e3), 1)
+            res.setdefault(run, {})[k] = e
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,0 +1,25 @@
+#!/bin/bash
+# rocprofv3 evidence for one round: kernel-trace stats of the bench and of the
+# FIR benchmark, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes (no
+# trace domains beside --pmc), summarised per kernel by scripts/pmc_summary.py.
+#   bash scripts/prof_round.sh r01   -> gpurun_out/prof/r01_*  (copy to profiles/)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+tag=${1:-r01}
+out=gpurun_out/prof/$tag
+mkdir -p $out
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-components"
+F="python3 scripts/firbench.py"
+run() {   # name, rocprof args..., -- cmd
+  local name=$1; shift
+  timeout -k 10 600 rocprofv3 "$@" > $out/$name.log 2>&1
+  local rc=$?; echo "$name rc=$rc"
+  [ $rc -eq 0 ] || { tail -5 $out/$name.log; exit $rc; }
+}
+run bench_trace --kernel-trace --stats --output-format csv -d $out/bench_trace -o bench -- $B
+run fir_trace --kernel-trace --stats --output-format csv -d $out/fir_trace -o fir -- $F
+run bench_fetch --pmc FETCH_SIZE --output-format csv -d $out/bench_fetch -o bench -- $B
+run bench_write --pmc WRITE_SIZE --output-format csv -d $out/bench_write -o bench -- $B
+run fir_fetch --pmc FETCH_SIZE --output-format csv -d $out/fir_fetch -o fir -- $F
+run fir_write --pmc WRITE_SIZE --output-format csv -d $out/fir_write -o fir -- $F
+python3 scripts/pmc_summary.py $out > $out/summary.json && cat $out/summary.json
