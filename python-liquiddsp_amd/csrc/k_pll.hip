@@ -285,13 +285,24 @@ __device__ __forceinline__ void load_sub(uint4 (&D)[4][2], const WalkBuf& b, int
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
 
-// Walk one candidate chunk (4 lane-blocks of 64 samples) from local sample
-// base0.  On entry dtheta(base0 + l) = K + l*DD (ldd = lane*DD); on exit K is
-// the offset at the chunk end (or at cnt for the last, partial chunk).
+// lane * m (mod 2^32) for a lane index (< 64): v_mul_i32_i24 when m fits 24
+// signed bits (the usual case), the quarter-rate v_mul_lo_u32 otherwise.
+__device__ __forceinline__ uint32_t lane_mul(uint32_t lane, uint32_t m)
+{
+    const int32_t ms = (int32_t)m;
+    if (ms >= -(1 << 23) && ms < (1 << 23)) return (uint32_t)__mul24((int)lane, ms);
+    return lane * m;
+}
+
+// Walker inner loop, latency-trimmed: per lane-block the offsets v = u + K + l DD
+// live in one VGPR that is updated in place after each repair
+// (v += (dk2 - j dk1) + l dk1), the direction-dependent record words are
+// selected per lane before the readlanes (3 instead of 6), and the rare
+// |di| > 1 case is tested with one scalar bit test.
 template <bool FULL>
-__device__ __forceinline__ void walk_sub(const uint4 (&D)[4][2], int base0, int cnt, uint32_t& K, uint32_t& DD,
-                                         uint32_t& ldd, float* __restrict__ yb, long sb, int lane, const FullCtx& fc,
-                                         unsigned long long& n_rep, int dbg)
+__device__ __forceinline__ void walk_sub2(const uint4 (&D)[4][2], int base0, int cnt, uint32_t& K, uint32_t& DD,
+                                          uint32_t& ldd, float* __restrict__ yb, long sb, int lane,
+                                          const FullCtx& fc, unsigned long long& n_rep)
 {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -301,27 +312,23 @@ __device__ __forceinline__ void walk_sub(const uint4 (&D)[4][2], int base0, int 
             nvalid = min(64, cnt - base);
             if (nvalid <= 0) return;
         }
-        const uint32_t u = D[q][0].y;
         unsigned long long M = (FULL || nvalid == 64) ? ~0ull : ((1ull << nvalid) - 1ull);
         unsigned long long PM = 0;
         uint32_t pout = 0;
-        if (dbg != 1) while (true) {
+        uint32_t v = D[q][0].y + K + lane_mul((uint32_t)lane, DD);
+        while (true) {
             // index of th + off equals index of th  <=>  u + off < 2^22 (mod 2^32)
-            const uint32_t v = u + K + ldd;
             const unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
             if (mask == 0) break;
             const int j = __builtin_ctzll(mask);
-            // side of the mismatch from two more ballots (SALU bit tests, no readlane of v)
-            const unsigned long long upm = __builtin_amdgcn_ballot_w64(v - 0x400000u < 0x400000u);   // di = +1
-            const unsigned long long dnm = __builtin_amdgcn_ballot_w64(v >= 0xffc00000u);           // di = -1
-            const bool up = (upm >> j) & 1ull;
-            const uint32_t a1 = rl(D[q][1].x, j), b1 = rl(D[q][0].z, j);
-            const uint32_t a2 = rl(D[q][1].y, j), b2 = rl(D[q][0].w, j);
-            const uint32_t ao = rl(D[q][1].w, j), bo = rl(D[q][1].z, j);
-            uint32_t dk1 = up ? a1 : b1;
-            uint32_t dk2 = up ? a2 : b2;
-            uint32_t ob = up ? ao : bo;
-            if (!up && !((dnm >> j) & 1ull)) {                 // rare: |di| > 1
+            const bool upl = v - 0x400000u < 0x400000u;                  // di = +1
+            const bool dnl = v >= 0xffc00000u;                          // di = -1
+            const unsigned long long bigm = __builtin_amdgcn_ballot_w64(!upl && !dnl);
+            const uint32_t sdk1 = upl ? D[q][1].x : D[q][0].z;
+            const uint32_t sdk2 = upl ? D[q][1].y : D[q][0].w;
+            const uint32_t sout = upl ? D[q][1].w : D[q][1].z;
+            uint32_t dk1 = rl(sdk1, j), dk2 = rl(sdk2, j), ob = rl(sout, j);
+            if ((bigm >> j) & 1ull) {                                   // rare: |di| > 1
                 const uint4 f = pll_full(fc, rl(D[q][0].x, j), rl(v, j) >> 22, sb + base + j);
                 dk1 = __builtin_amdgcn_readfirstlane(f.x);
                 dk2 = __builtin_amdgcn_readfirstlane(f.y);
@@ -330,15 +337,17 @@ __device__ __forceinline__ void walk_sub(const uint4 (&D)[4][2], int base0, int 
             n_rep++;
             pout = lane == j ? ob : pout;
             PM |= 1ull << j;
-            K = __builtin_amdgcn_readfirstlane(K + dk2 - (uint32_t)j * dk1);   // scalar state
-            DD = __builtin_amdgcn_readfirstlane(DD + dk1);
-            ldd = (uint32_t)lane * DD;
+            const uint32_t c = dk2 - (uint32_t)j * dk1;
+            K += c;
+            DD += dk1;
+            v += c + lane_mul((uint32_t)lane, dk1);
             M &= (~0ull << j) << 1;
         }
         if (PM != 0 && ((PM >> lane) & 1ull)) yb[base + lane] = __uint_as_float(pout);
         K += (uint32_t)nvalid * DD;
-        if (!FULL && nvalid < 64) return;
+        if (!FULL && nvalid < 64) break;
     }
+    ldd = lane_mul((uint32_t)lane, DD);
 }
 
 // Wave 0 walks block c; waves 1-7 store block c+1 (fetched into registers
@@ -369,7 +378,6 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     fc.beta = st->beta;
     fc.mod_index = in.mod_index;
     uint32_t th_t = st->theta, d_t = st->dtheta;      // true state at the current block start
-    const int dbgw = __builtin_amdgcn_readfirstlane(cb.dbg);
     unsigned long long n_rep = 0, cyc_walk = 0, cyc_wait = 0;
     for (long c = 0; c < nblk; c++) {
         const unsigned long long t0 = wall_clock64();
@@ -401,10 +409,10 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                     }
                     if (sub & 1) {
                         if (sub + 1 < kSub) load_sub(D0, b, sub + 1, lane);
-                        walk_sub<true>(D1, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, dbgw);
+                        walk_sub2<true>(D1, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep);
                     } else {
                         if (sub + 1 < kSub) load_sub(D1, b, sub + 1, lane);
-                        walk_sub<true>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, dbgw);
+                        walk_sub2<true>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep);
                     }
                 }
                 last = kSub - 1;
@@ -416,7 +424,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                         ldd = (uint32_t)lane * DD;
                     }
                     load_sub(D0, b, sub, lane);
-                    walk_sub<false>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, dbgw);
+                    walk_sub2<false>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep);
                     last = sub;
                 }
             }
