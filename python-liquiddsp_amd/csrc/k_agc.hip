@@ -78,6 +78,45 @@ __device__ __forceinline__ float2 agc_step(AgcReg& r, const AgcState& p, float2 
     return y;
 }
 
+// Approximate step (hardware v_log_f32 / v_exp_f32, float32 smoothing): used
+// only to bring a chunk's guessed state within a few ulps of the true
+// trajectory before the exact warm-up (never for outputs).
+__device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, float2 x)
+{
+    const float a = x.x * r.g, b = x.y * r.g;
+    const float y2 = a * a - b * (-b);
+    // the smoothing exactly as agc_step: its float32 rounding would bias y2p (error ~1 ulp / alpha)
+    r.y2p = (float)((1.0 - (double)p.alpha) * (double)r.y2p + (double)(p.alpha * y2));
+    if (!p.locked) {
+        // g *= expf(-0.5 alpha ln y2p) with the exact loop's rounding structure (factor
+        // rounded to float, then one float multiply): ln from v_log_f32 (its error is
+        // scaled by alpha/2, far below an ulp of the factor), exp by a short series.  The
+        // factor then rounds like lm_expf's almost always, so this trajectory tracks the
+        // exact one within a few ulps instead of drifting by its own rounding noise.
+        if (r.y2p > 1e-6f) {
+            const float t = -0.5f * p.alpha * (__builtin_amdgcn_logf(r.y2p) * 0.69314718056f);
+            const float u = t * (1.0f + t * (0.5f + t * (0.16666667f + t * 0.041666668f)));
+            r.g *= 1.0f + u;
+        }
+        r.g = (r.g > 1e6f) ? 1e6f : r.g;
+        agc_squelch(r, p);
+    }
+}
+
+__device__ __forceinline__ void agc_run_approx(AgcReg& r, const AgcState& p, const float2* __restrict__ x, long a,
+                                               long b)
+{
+    constexpr int kA = 8;
+    for (long i = a; i < b; i += kA) {
+        float2 cx[kA];
+#pragma unroll
+        for (int j = 0; j < kA; j++) cx[j] = x[min(i + j, b - 1)];
+#pragma unroll
+        for (int j = 0; j < kA; j++)
+            if (i + j < b) agc_step_approx(r, p, cx[j]);
+    }
+}
+
 // Run the AGC over x[a, b) with the loads software-pipelined kB samples ahead
 // (they are off the gain recurrence's dependence chain).  OUT: write y/status.
 constexpr int kB = 8;
@@ -125,12 +164,17 @@ __global__ void k_agc_seq(const float2* __restrict__ x, long n, AgcState* st, fl
     st->timer = r.timer;
 }
 
-// scratch: [nchunks][2 (guess, end)][4 words: g, y2p, mode, timer]
-// Chunk k starts W samples early from a guessed state: y2p = 1 and the gain
-// that normalises the mean power of the kPow samples before the warm-up.
+// scratch: [nchunks][2 (start, end)][4 words: g, y2p, mode, timer]
+// Chunk k's exact run starts W samples early (w0 = s0 - W) from a guessed
+// state.  The guess comes from an approximate pass (agc_step_approx) over the
+// Wa samples before w0, itself started from y2p = 1 and the gain that
+// normalises the mean power of the kPow samples before it; that brings the
+// guess within a few ulps of the true trajectory, so the exact float32 loop
+// coalesces bit for bit within ~100 samples typically (a few thousand at
+// worst; chunks that have not are re-run by k_agc_fix / k_agc_verify).
 constexpr int kPow = 256;
 __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x, long n, const AgcState* st, int C,
-                                                   int W, long nch, unsigned* __restrict__ sc,
+                                                   int W, int Wa, long nch, unsigned* __restrict__ sc,
                                                    float2* __restrict__ y, uint8_t* __restrict__ status)
 {
     const long chunk = (long)blockIdx.x * 64 + threadIdx.x;
@@ -143,30 +187,37 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
         w0 = 0;
         r = AgcReg{p.g, p.y2p, p.mode, p.timer};
     } else {
-        r.y2p = 1.0f;
-        r.mode = (p.mode == SQ_DISABLED) ? SQ_DISABLED : SQ_ENABLED;
-        r.timer = 0;
-        if (p.locked) {
-            r.g = p.g;                          // gain frozen while locked
+        long a0 = w0 - Wa;
+        if (a0 <= 0) {
+            a0 = 0;
+            r = AgcReg{p.g, p.y2p, p.mode, p.timer};
         } else {
-            const long a = max(0L, w0 - kPow);
-            const long m = w0 - a;
-            double pw = 0.0;
-            if (m > 0) {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0};
-                for (long i = a; i < w0; i += 16) {
-                    float2 v[16];
+            r.y2p = 1.0f;
+            r.mode = (p.mode == SQ_DISABLED) ? SQ_DISABLED : SQ_ENABLED;
+            r.timer = 0;
+            if (p.locked) {
+                r.g = p.g;                          // gain frozen while locked
+            } else {
+                const long a = max(0L, a0 - kPow);
+                const long m = a0 - a;
+                double pw = 0.0;
+                if (m > 0) {
+                    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+                    for (long i = a; i < a0; i += 16) {
+                        float2 v[16];
 #pragma unroll
-                    for (int j = 0; j < 16; j++) v[j] = x[min(i + j, w0 - 1)];
+                        for (int j = 0; j < 16; j++) v[j] = x[min(i + j, a0 - 1)];
 #pragma unroll
-                    for (int j = 0; j < 16; j++)
-                        if (i + j < w0) acc[j & 3] += (double)v[j].x * v[j].x + (double)v[j].y * v[j].y;
+                        for (int j = 0; j < 16; j++)
+                            if (i + j < a0) acc[j & 3] += (double)v[j].x * v[j].x + (double)v[j].y * v[j].y;
+                    }
+                    pw = (acc[0] + acc[1] + acc[2] + acc[3]) / (double)m;
                 }
-                pw = (acc[0] + acc[1] + acc[2] + acc[3]) / (double)m;
+                const double g = pw > 1e-12 ? 1.0 / sqrt(pw) : 1e6;
+                r.g = (float)(g > 1e6 ? 1e6 : g);
             }
-            const double g = pw > 1e-12 ? 1.0 / sqrt(pw) : 1e6;
-            r.g = (float)(g > 1e6 ? 1e6 : g);
         }
+        agc_run_approx(r, p, x, a0, w0);
     }
     agc_run<false>(r, p, x, w0, s0, y, status);
     unsigned* gs = sc + chunk * 8;
@@ -181,9 +232,43 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
     gs[7] = r.timer;
 }
 
+// Parallel repair round: every chunk of the given parity whose start state
+// differs from its predecessor's end state re-runs from that end state
+// (in place; the predecessors have the other parity, so nothing they hold
+// changes during the launch).  Chunks that start from the true state
+// (s0 <= W) are exact already.
+__global__ void __launch_bounds__(64) k_agc_fix(const float2* __restrict__ x, long n, const AgcState* st, int C,
+                                                int W, long nch, int parity, unsigned* __restrict__ sc,
+                                                float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg)
+{
+    const long chunk = ((long)blockIdx.x * 64 + threadIdx.x) * 2 + parity;
+    if (chunk < 1 || chunk >= nch || chunk * C - W <= 0) return;
+    unsigned* gs = sc + chunk * 8;
+    const unsigned* pe = sc + (chunk - 1) * 8 + 4;
+    unsigned e[4];
+    bool same = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        e[i] = pe[i];
+        same &= e[i] == gs[i];
+    }
+    if (same) return;
+    if (dbg) atomicAdd(dbg, 1u);
+    const AgcState p = *st;
+    AgcReg r{__uint_as_float(e[0]), __uint_as_float(e[1]), (int)e[2], e[3]};
+    const long s0 = chunk * C;
+    agc_run<true>(r, p, x, s0, min(n, s0 + C), y, status);
+#pragma unroll
+    for (int i = 0; i < 4; i++) gs[i] = e[i];
+    gs[4] = __float_as_uint(r.g);
+    gs[5] = __float_as_uint(r.y2p);
+    gs[6] = (unsigned)r.mode;
+    gs[7] = r.timer;
+}
+
 __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x, long n, AgcState* st, int C, int W,
                                                    long nch, unsigned* __restrict__ sc, float2* __restrict__ y,
-                                                   uint8_t* __restrict__ status)
+                                                   uint8_t* __restrict__ status, unsigned* dbg)
 {
     const int lane = threadIdx.x;
     const AgcState p = *st;
@@ -207,6 +292,7 @@ __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x,
             const unsigned* e = sc + (kb - 1) * 8 + 4;
             AgcReg r{__uint_as_float(ldntu(e)), __uint_as_float(ldntu(e + 1)), (int)ldntu(e + 2), ldntu(e + 3)};
             agc_run<true>(r, p, x, kb * C, min(n, kb * C + C), y, status);
+            if (dbg) dbg[0]++;
             unsigned* en = sc + kb * 8;
             en[4] = __float_as_uint(r.g);
             en[5] = __float_as_uint(r.y2p);
@@ -261,13 +347,22 @@ void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y,
     {
         LDSP_PROF(s, "k_agc_chunks");
         hipLaunchKernelGGL(k_agc_chunks, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, (const float2*)x,
-                           (long)n, (const AgcState*)st, p.C, p.W, p.nchunks, (unsigned*)p.scratch, (float2*)y, status);
+                           (long)n, (const AgcState*)st, p.C, p.W, p.Wa, p.nchunks, (unsigned*)p.scratch, (float2*)y,
+                           status);
     }
+    LDSP_HIP(hipGetLastError());
+    for (int round = 0; round < p.rounds; round++)
+        for (int parity = 1; parity >= 0; parity--) {
+            LDSP_PROF(s, "k_agc_fix");
+            hipLaunchKernelGGL(k_agc_fix, dim3((unsigned)((p.nchunks / 2 + 64) / 64)), dim3(64), 0, s,
+                               (const float2*)x, (long)n, (const AgcState*)st, p.C, p.W, p.nchunks, parity,
+                               (unsigned*)p.scratch, (float2*)y, status, p.dbg ? p.dbg + round : nullptr);
+        }
     LDSP_HIP(hipGetLastError());
     {
         LDSP_PROF(s, "k_agc_verify");
         hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, p.nchunks,
-                           (unsigned*)p.scratch, (float2*)y, status);
+                           (unsigned*)p.scratch, (float2*)y, status, p.dbg ? p.dbg + p.rounds : nullptr);
     }
     LDSP_HIP(hipGetLastError());
 }

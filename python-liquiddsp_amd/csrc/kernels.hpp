@@ -105,7 +105,10 @@ void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, cons
 // start state differs bit-wise from its predecessor's end state.
 struct SpecPlan {
     int C;                // samples per chunk
-    int W;                // warm-up samples
+    int W;                // warm-up samples (exact)
+    int Wa = 0;           // AGC: approximate warm-up before the exact one
+    int rounds = 0;       // AGC: parallel repair rounds before the sequential verifier
+    unsigned* dbg = nullptr;   // AGC debug: per-round re-run counters (LDSP_DEBUG_AGC)
     long nchunks;
     void* scratch;        // device scratch (states: start-guess and end per chunk)
 };
