@@ -1513,7 +1513,7 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
             float* mbuf = q->suppressed ? dy : (float*)q->mb.ensure(n * 4, q->device);
             void* pscr = q->pll.ensure(k::pll_scratch_bytes(n), q->device);
             k::ampmodem_pll(x0, dx, q->dlh[q->cur].p, q->dlh[1 - q->cur].p, (int)q->m, n, q->dst.as<k::AmpState>(),
-                            q->dtab.as<float>(), q->mod_index, q->suppressed ? 1 : 0, mbuf, pscr, e.stream);
+                            q->dtab.as<float>(), q->mod_index, q->suppressed ? 1 : 0, q->st.alpha, mbuf, pscr, e.stream);
             if (n >= 8192 && std::getenv("LDSP_DEBUG_PLL")) {
                 unsigned long long stt[4];
                 LDSP_HIP(hipMemcpyAsync(stt, (char*)pscr + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,

@@ -40,7 +40,7 @@ namespace {
 constexpr int kBlk = 1024;        // walker block
 constexpr int kCand = 256;        // candidate chunk
 constexpr int kSub = kBlk / kCand;
-constexpr int kWarm = 2048;       // candidate warm-up
+constexpr int kWarm = 1024;       // candidate warm-up (locks the loop; 2048 gives no fewer repairs)
 
 __device__ __forceinline__ uint32_t tidx(uint32_t th) { return ((th + (1u << 21)) >> 22) & 0x3ffu; }
 
@@ -188,7 +188,7 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
 }
 
 __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpState* st, long nchc, CandBuf cb,
-                                                 float* __restrict__ y)
+                                                 float* __restrict__ y, int warm)
 {
     __shared__ float tab[1024];
     for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = in.table[i];
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpStat
     const long s0 = k * kCand, s1 = min(n, s0 + kCand);
     const float alpha = st->alpha, beta = st->beta;
     uint32_t theta = st->theta, d = st->dtheta;
-    long w0 = s0 - kWarm;
+    long w0 = s0 - warm;
     if (w0 <= 0) {
         w0 = 0;                                       // exact: from the true state
     } else {
@@ -350,8 +350,75 @@ __device__ __forceinline__ void walk_sub2(const uint4 (&D)[4][2], int base0, int
     ldd = lane_mul((uint32_t)lane, DD);
 }
 
+// v + lane * dk1.  F24: every kick difference fits 24 signed bits (host check:
+// |k1| <= alpha 2^31, so |dk1| < 2^23 when alpha <= 2^-9), one v_mad_i32_i24.
+template <bool F24>
+__device__ __forceinline__ uint32_t mad_lane(uint32_t lane, uint32_t dk1, uint32_t v)
+{
+    if (F24) {
+        uint32_t r;
+        asm volatile("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(lane), "s"(dk1), "v"(v));
+        return r;
+    }
+    return v + lane * dk1;
+}
+
+// Repair loop with the fewest dependent instructions found: mismatch / +1 /
+// |di| > 1 classes from three compares, direction-selected record words read
+// back with three readlanes, the patched output written into lane j with
+// v_writelane, the per-lane offset advanced with one 24-bit multiply-add.
+template <bool FULL, bool F24>
+__device__ __forceinline__ void walk_sub3(const uint4 (&D)[4][2], int base0, int cnt, uint32_t& K, uint32_t& DD,
+                                          uint32_t& ldd, float* __restrict__ yb, long sb, int lane,
+                                          const FullCtx& fc, unsigned long long n_rep, unsigned& nrep)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int base = base0 + q * 64;
+        int nvalid = 64;
+        if (!FULL) {
+            nvalid = min(64, cnt - base);
+            if (nvalid <= 0) return;
+        }
+        unsigned long long M = (FULL || nvalid == 64) ? ~0ull : ((1ull << nvalid) - 1ull);
+        unsigned long long PM = 0;
+        uint32_t pout = 0;
+        uint32_t v = D[q][0].y + K + ldd;                // ldd = lane * DD (mod 2^32)
+        unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
+        if (n_rep == 1) mask = 0;      // timing experiment (LDSP_DEBUG_PLL_MODE=1): skip repairs
+        while (mask != 0) {
+            const int j = __builtin_ctzll(mask);
+            const unsigned long long bigm = __builtin_amdgcn_ballot_w64(v + 0x400000u > 0xbfffffu);
+            const bool upl = v - 0x400000u < 0x400000u;                  // di = +1 (else -1)
+            const uint32_t sdk1 = upl ? D[q][1].x : D[q][0].z;
+            const uint32_t sdk2 = upl ? D[q][1].y : D[q][0].w;
+            const uint32_t sout = upl ? D[q][1].w : D[q][1].z;
+            uint32_t dk1 = rl(sdk1, j), dk2 = rl(sdk2, j), ob = rl(sout, j);
+            if (__builtin_expect((bigm >> j) & 1ull, 0)) {              // rare: |di| > 1
+                const uint4 f = pll_full(fc, rl(D[q][0].x, j), rl(v, j) >> 22, sb + base + j);
+                dk1 = __builtin_amdgcn_readfirstlane(f.x);
+                dk2 = __builtin_amdgcn_readfirstlane(f.y);
+                ob = __builtin_amdgcn_readfirstlane(f.z);
+            }
+            asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(pout) : "s"(ob), "s"(j) : "m0");
+            PM |= 1ull << j;
+            K += dk2 - (uint32_t)j * dk1;
+            DD += dk1;
+            nrep++;
+            ldd = mad_lane<F24>((uint32_t)lane, dk1, ldd);
+            v = D[q][0].y + K + ldd;
+            M &= (~0ull << j) << 1;
+            mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
+        }
+        if ((PM >> lane) & 1ull) yb[base + lane] = __uint_as_float(pout);
+        K += (uint32_t)nvalid * DD;
+        if (!FULL && nvalid < 64) break;
+    }
+}
+
 // Wave 0 walks block c; waves 1-7 store block c+1 (fetched into registers
 // during the previous block) into the other LDS buffer and fetch block c+2.
+template <bool F24>
 __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, long nblk, CandBuf cb,
                                                            float* __restrict__ y)
 {
@@ -378,7 +445,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     fc.beta = st->beta;
     fc.mod_index = in.mod_index;
     uint32_t th_t = st->theta, d_t = st->dtheta;      // true state at the current block start
-    unsigned long long n_rep = 0, cyc_walk = 0, cyc_wait = 0;
+    unsigned long long n_rep = (unsigned long long)__builtin_amdgcn_readfirstlane(cb.dbg), cyc_walk = 0, cyc_wait = 0;
+    unsigned nrep = 0;
     for (long c = 0; c < nblk; c++) {
         const unsigned long long t0 = wall_clock64();
         if (wave != 0) {
@@ -393,8 +461,10 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             float* yb = y + s0;
             // Offset of the true trajectory from the candidate (exact, mod 2^32):
             // at local sample base + l of the current lane-block, dtheta = K + l*DD.
-            uint32_t K = th_t - b.cs[0];
-            uint32_t DD = d_t - b.cs[1];
+            // candidate chunk start / end states of the block (cs[0..7], ce[0..7]) in one LDS read
+            const uint32_t csce = lane < 2 * kSub ? b.cs[lane] : (lane < 4 * kSub ? b.ce[lane - 2 * kSub] : 0u);
+            uint32_t K = th_t - rl(csce, 0);
+            uint32_t DD = d_t - rl(csce, 1);
             uint32_t ldd = (uint32_t)lane * DD;
             uint4 D0[4][2], D1[4][2];
             load_sub(D0, b, 0, lane);
@@ -403,37 +473,42 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
 #pragma unroll
                 for (int sub = 0; sub < kSub; sub++) {
                     if (sub > 0) {                                  // next candidate chunk: rebase the offset
-                        K = b.ce[2 * sub - 2] + K - b.cs[2 * sub];
-                        DD = b.ce[2 * sub - 1] + DD - b.cs[2 * sub + 1];
+                        K = rl(csce, 2 * kSub + 2 * sub - 2) + K - rl(csce, 2 * sub);
+                        DD = rl(csce, 2 * kSub + 2 * sub - 1) + DD - rl(csce, 2 * sub + 1);
                         ldd = (uint32_t)lane * DD;
                     }
                     if (sub & 1) {
                         if (sub + 1 < kSub) load_sub(D0, b, sub + 1, lane);
-                        walk_sub2<true>(D1, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep);
+                        walk_sub3<true, F24>(D1, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, nrep);
                     } else {
                         if (sub + 1 < kSub) load_sub(D1, b, sub + 1, lane);
-                        walk_sub2<true>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep);
+                        walk_sub3<true, F24>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, nrep);
                     }
                 }
                 last = kSub - 1;
             } else {
                 for (int sub = 0; sub * kCand < cnt; sub++) {
                     if (sub > 0) {
-                        K = b.ce[2 * sub - 2] + K - b.cs[2 * sub];
-                        DD = b.ce[2 * sub - 1] + DD - b.cs[2 * sub + 1];
+                        K = rl(csce, 2 * kSub + 2 * sub - 2) + K - rl(csce, 2 * sub);
+                        DD = rl(csce, 2 * kSub + 2 * sub - 1) + DD - rl(csce, 2 * sub + 1);
                         ldd = (uint32_t)lane * DD;
                     }
                     load_sub(D0, b, sub, lane);
-                    walk_sub2<false>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep);
+                    walk_sub3<false, F24>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, nrep);
                     last = sub;
                 }
             }
             // true state at the block end = candidate end + offset at cnt
             th_t = b.ce[2 * last] + K;
             d_t = b.ce[2 * last + 1] + DD;
+            (void)csce;
         }
+        // LDS-only barrier: __syncthreads() would also drain the loaders' global fetch of
+        // block c + 2 (vmcnt(0)), putting an HBM round trip into every block
         const unsigned long long t1 = wall_clock64();
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const unsigned long long t2 = wall_clock64();
         cyc_walk += t1 - t0;
         cyc_wait += t2 - t1;
@@ -441,7 +516,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     if (tid == 0) {
         st->theta = th_t;
         st->dtheta = d_t;
-        cb.stats[0] = n_rep;
+        cb.stats[0] = nrep;
         cb.stats[1] = 0;
         cb.stats[2] = cyc_walk;
         cb.stats[3] = cyc_wait;
@@ -473,7 +548,8 @@ size_t pll_stats_offset(size_t n)
 }
 
 void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_out, int m, size_t n, AmpState* st,
-                  const float* table, float mod_index, int costas, float* y, void* scratch, hipStream_t s)
+                  const float* table, float mod_index, int costas, float alpha_host, float* y, void* scratch,
+                  hipStream_t s)
 {
     if (n == 0) return;
     PllIn in;
@@ -504,13 +580,17 @@ void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_ou
         cb.dbg = dbg_mode;
         {
             LDSP_PROF(s, "k_pll_cand");
+            static const int warm = std::getenv("LDSP_PLL_WARM") ? std::atoi(std::getenv("LDSP_PLL_WARM")) : kWarm;
             hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((nchc + 63) / 64)), dim3(64), 0, s, in, (long)n,
-                               (const AmpState*)st, nchc, cb, y);
+                               (const AmpState*)st, nchc, cb, y, warm);
         }
         LDSP_HIP(hipGetLastError());
         {
             LDSP_PROF(s, "k_pll_walk");
-            hipLaunchKernelGGL(k_pll_walk, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
+            if (alpha_host <= 1.0f / 512.0f)
+                hipLaunchKernelGGL(k_pll_walk<true>, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
+            else
+                hipLaunchKernelGGL(k_pll_walk<false>, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
         }
         LDSP_HIP(hipGetLastError());
     }

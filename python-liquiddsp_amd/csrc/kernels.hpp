@@ -138,7 +138,7 @@ struct AmpState {         // device-resident PLL state
 size_t pll_scratch_bytes(size_t n);
 size_t pll_stats_offset(size_t n);     // 4 x u64 walker counters inside the scratch (debug)
 void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_out, int m, size_t n,
-                  AmpState* st, const float* table, float mod_index, int costas, float* y, void* scratch,
+                  AmpState* st, const float* table, float mod_index, int costas, float alpha_host, float* y, void* scratch,
                   hipStream_t s);
 
 // ------------------------------------------------------------------ debug
