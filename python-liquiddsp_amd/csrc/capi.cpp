@@ -1229,9 +1229,9 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
                 q->state_to(false, e.stream);
                 k::SpecPlan p;
                 p.W = q->spec_W;
-                p.C = std::max(256, q->spec_W);
+                p.C = 128;                       // chunks are cheap: W + C steps per lane
                 p.nchunks = (long)((n + p.C - 1) / p.C);
-                const size_t need = (size_t)p.nchunks * 2 * q->ncomp() * q->fsz() * sizeof(float);
+                const size_t need = k::spec_scratch_bytes(p.nchunks, q->ncomp(), q->fsz());
                 p.scratch = q->sc1.ensure(need, q->device);
                 k::iir_spec(q->cplx, d, dx, n, q->st32.as<float>(), p, dy, e.stream);
             } else if (q->mode == LDSP_MODE_EXACT) {
@@ -1409,7 +1409,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
                 p.rounds = 3;
                 p.C = 256;
                 p.nchunks = (long)((n + p.C - 1) / p.C);
-                p.scratch = q->scratch.ensure(((size_t)p.nchunks * 8 + 8) * sizeof(unsigned), q->device);
+                p.scratch = q->scratch.ensure(k::agc_scratch_bytes(p.nchunks), q->device);
                 static const bool dbg = std::getenv("LDSP_DEBUG_AGC") != nullptr;
                 if (dbg) {
                     p.dbg = (unsigned*)p.scratch + (size_t)p.nchunks * 8;

@@ -266,28 +266,59 @@ __global__ void __launch_bounds__(64) k_agc_fix(const float2* __restrict__ x, lo
     gs[7] = r.timer;
 }
 
+// Parallel pre-check: bit c of flags[c / 64] = chunk c's start state differs
+// from chunk c-1's end state (after the repair rounds).
+__global__ void __launch_bounds__(64) k_agc_flags(int C, int W, long nch, const unsigned* __restrict__ sc,
+                                                  unsigned long long* __restrict__ flags)
+{
+    const long kk = (long)blockIdx.x * 64 + threadIdx.x;
+    bool bad = false;
+    if (kk >= 1 && kk < nch && kk * C - W > 0) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) bad |= sc[kk * 8 + i] != sc[(kk - 1) * 8 + 4 + i];
+    }
+    const unsigned long long m = __ballot(bad);
+    if (threadIdx.x == 0) flags[blockIdx.x] = m;
+}
+
 __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x, long n, AgcState* st, int C, int W,
-                                                   long nch, unsigned* __restrict__ sc, float2* __restrict__ y,
+                                                   long nch, unsigned* __restrict__ sc,
+                                                   const unsigned long long* __restrict__ flags, float2* __restrict__ y,
                                                    uint8_t* __restrict__ status, unsigned* dbg)
 {
     const int lane = threadIdx.x;
     const AgcState p = *st;
+    const long nw = (nch + 63) / 64;
     long k = 1;
+    bool direct = false;          // chunk k's predecessor was re-run: compare states, not its flag
     while (k < nch) {
-        const long kk = k + lane;
-        bool bad = false;
-        if (kk < nch && kk * C - W > 0) {
-            const unsigned* g = sc + kk * 8;
-            const unsigned* e = sc + (kk - 1) * 8 + 4;
-#pragma unroll
-            for (int i = 0; i < 4; i++) bad |= ldntu(g + i) != ldntu(e + i);
+        long kb;
+        if (direct) {
+            bool bad = false;
+            if (k * C - W > 0 && lane < 4) bad = ldntu(sc + k * 8 + lane) != ldntu(sc + (k - 1) * 8 + 4 + lane);
+            if (__ballot(bad) == 0) {
+                direct = false;
+                k++;
+                continue;
+            }
+            kb = k;
+        } else {
+            // flags of 64 x 64 chunks per step (k_agc_flags)
+            const long wk = k >> 6;
+            unsigned long long w = (wk + lane < nw) ? flags[wk + lane] : 0ull;
+            if (lane == 0) w &= ~0ull << (k & 63);
+            const unsigned long long bm = __ballot(w != 0ull);
+            if (bm == 0) {
+                k = (wk + 64) << 6;
+                continue;
+            }
+            const int L = __builtin_ctzll(bm);
+            const unsigned long long wd =
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w >> 32), L) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, L);
+            kb = ((wk + L) << 6) + __builtin_ctzll(wd);
+            if (kb >= nch) break;
         }
-        const unsigned long long m = __ballot(bad);
-        if (m == 0) {
-            k += 64;
-            continue;
-        }
-        const long kb = k + __ffsll((long long)m) - 1;
         if (lane == 0) {
             const unsigned* e = sc + (kb - 1) * 8 + 4;
             AgcReg r{__uint_as_float(ldntu(e)), __uint_as_float(ldntu(e + 1)), (int)ldntu(e + 2), ldntu(e + 3)};
@@ -302,6 +333,7 @@ __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         k = kb + 1;
+        direct = true;
     }
     if (lane == 0) {
         const unsigned* e = sc + (nch - 1) * 8 + 4;
@@ -341,6 +373,9 @@ void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hi
     LDSP_HIP(hipGetLastError());
 }
 
+size_t agc_flags_offset_words(long nchunks) { return (size_t)nchunks * 8 + 8; }     // after records + debug words
+size_t agc_scratch_bytes(long nchunks) { return (agc_flags_offset_words(nchunks) + 2 * ((nchunks + 63) / 64 + 64)) * 4; }
+
 void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
@@ -359,10 +394,18 @@ void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y,
                                (unsigned*)p.scratch, (float2*)y, status, p.dbg ? p.dbg + round : nullptr);
         }
     LDSP_HIP(hipGetLastError());
+    unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
+    {
+        LDSP_PROF(s, "k_agc_flags");
+        hipLaunchKernelGGL(k_agc_flags, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, p.C, p.W, p.nchunks,
+                           (const unsigned*)p.scratch, flags);
+    }
+    LDSP_HIP(hipGetLastError());
     {
         LDSP_PROF(s, "k_agc_verify");
         hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, p.nchunks,
-                           (unsigned*)p.scratch, (float2*)y, status, p.dbg ? p.dbg + p.rounds : nullptr);
+                           (unsigned*)p.scratch, (const unsigned long long*)flags, (float2*)y, status,
+                           p.dbg ? p.dbg + p.rounds : nullptr);
     }
     LDSP_HIP(hipGetLastError());
 }

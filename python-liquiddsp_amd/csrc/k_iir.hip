@@ -138,6 +138,35 @@ __global__ void k_iir_seq(IirDesc d, const float* __restrict__ x, long n, int nc
     }
 }
 
+// x[a, b) of component c through a float32 step, loads batched 8 ahead (off the
+// recurrence's dependence chain); WRITE stores the outputs.
+template <bool WRITE, class StepF>
+__device__ __forceinline__ void run_f32(StepF&& step, const float* __restrict__ x, float* __restrict__ y, long a,
+                                        long b, int ncomp, int c)
+{
+    constexpr int kQ = 8;
+    if (a >= b) return;
+    float nx[kQ];
+#pragma unroll
+    for (int j = 0; j < kQ; j++) nx[j] = x[min(a + j, b - 1) * ncomp + c];
+    for (long i = a; i < b; i += kQ) {
+        float cx[kQ];
+#pragma unroll
+        for (int j = 0; j < kQ; j++) cx[j] = nx[j];
+        if (i + kQ < b) {
+#pragma unroll
+            for (int j = 0; j < kQ; j++) nx[j] = x[min(i + kQ + j, b - 1) * ncomp + c];
+        }
+#pragma unroll
+        for (int j = 0; j < kQ; j++) {
+            if (i + j < b) {
+                const float o = step(cx[j]);
+                if (WRITE) y[(i + j) * ncomp + c] = o;
+            }
+        }
+    }
+}
+
 // --------------------------------------------------------------- speculative exact
 // scratch layout: [nchunks][2 (guess, end)][ncomp][fstate]  + flags
 __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* __restrict__ x, long n, int ncomp,
@@ -164,13 +193,13 @@ __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* 
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
             for (int k = 0; k < 3; k++) v[s][k] = (from_true && s < d.nsos) ? state0[c * fs + 3 * s + k] : 0.0f;
-        for (long i = w0; i < s0; i++) (void)sos_step(cf, v, x[i * ncomp + c]);
+        run_f32<false>([&](float u) { return sos_step(cf, v, u); }, x, y, w0, s0, ncomp, c);
 #pragma unroll
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
             for (int k = 0; k < 3; k++)
                 if (s < d.nsos) guess[3 * s + k] = v[s][k];
-        for (long i = s0; i < s1; i++) y[i * ncomp + c] = sos_step(cf, v, x[i * ncomp + c]);
+        run_f32<true>([&](float u) { return sos_step(cf, v, u); }, x, y, s0, s1, ncomp, c);
 #pragma unroll
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
@@ -182,11 +211,11 @@ __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* 
         float v[kMaxTf];
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++) v[i] = (from_true && i < d.nv) ? state0[c * fs + i] : 0.0f;
-        for (long i = w0; i < s0; i++) (void)tf_step(cf, v, x[i * ncomp + c]);
+        run_f32<false>([&](float u) { return tf_step(cf, v, u); }, x, y, w0, s0, ncomp, c);
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++)
             if (i < d.nv) guess[i] = v[i];
-        for (long i = s0; i < s1; i++) y[i * ncomp + c] = tf_step(cf, v, x[i * ncomp + c]);
+        run_f32<true>([&](float u) { return tf_step(cf, v, u); }, x, y, s0, s1, ncomp, c);
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++)
             if (i < d.nv) endst[i] = v[i];
@@ -196,29 +225,69 @@ __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* 
 // Verifier: one wave walks the chunks in order.  Chunk k's outputs are exact
 // iff its guessed start state equals chunk k-1's (exact) end state bit for bit
 // (chunks whose warm-up reached the call start began from the true state).
+// Parallel pre-check: bit c of flags[c / 64] = chunk c's guessed start state
+// differs from chunk c-1's end state (before any re-run).
+__global__ void __launch_bounds__(64) k_iir_spec_flags(IirDesc d, int ncomp, int C, int W, long nch,
+                                                       const float* __restrict__ sc,
+                                                       unsigned long long* __restrict__ flags)
+{
+    const int fs = fstate_size(d);
+    const int per = ncomp * fs;
+    const long kk = (long)blockIdx.x * 64 + threadIdx.x;
+    bool bad = false;
+    if (kk >= 1 && kk < nch && kk * C - W > 0) {
+        const float* g = sc + (kk * 2 + 0) * per;
+        const float* e = sc + ((kk - 1) * 2 + 1) * per;
+        for (int i = 0; i < per; i++) bad |= __float_as_uint(g[i]) != __float_as_uint(e[i]);
+    }
+    const unsigned long long m = __ballot(bad);
+    if (threadIdx.x == 0) flags[blockIdx.x] = m;
+}
+
+__device__ __forceinline__ uint32_t rl_u32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
+
 __global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* __restrict__ x, long n, int ncomp,
                                                         int C, int W, long nch, float* __restrict__ sc,
+                                                        const unsigned long long* __restrict__ flags,
                                                         float* __restrict__ state, float* __restrict__ y)
 {
     const int lane = threadIdx.x;
     const int fs = fstate_size(d);
     const int per = ncomp * fs;   // floats per (chunk, kind)
+    const long nw = (nch + 63) / 64;
     long k = 1;
+    bool direct = false;          // chunk k's predecessor was re-run: compare states, not its flag
     while (k < nch) {
-        // lanes check chunks k .. k+63
-        const long kk = k + lane;
-        bool bad = false;
-        if (kk < nch && kk * C - W > 0) {
-            const float* g = sc + (kk * 2 + 0) * per;
-            const float* e = sc + ((kk - 1) * 2 + 1) * per;
-            for (int i = 0; i < per; i++) bad |= (__float_as_uint(ldnt(g + i)) != __float_as_uint(ldnt(e + i)));
+        long kb;
+        if (direct) {
+            bool bad = false;
+            if (k * C - W > 0 && lane < per) {
+                const float* g = sc + (k * 2 + 0) * per;
+                const float* e = sc + ((k - 1) * 2 + 1) * per;
+                bad = __float_as_uint(ldnt(g + lane)) != __float_as_uint(ldnt(e + lane));
+            }
+            if (__ballot(bad) == 0) {
+                direct = false;
+                k++;
+                continue;
+            }
+            kb = k;
+        } else {
+            // flags of 64 x 64 chunks per step (k_iir_spec_flags)
+            const long wk = k >> 6;
+            unsigned long long w = (wk + lane < nw) ? flags[wk + lane] : 0ull;
+            if (lane == 0) w &= ~0ull << (k & 63);
+            const unsigned long long bm = __ballot(w != 0ull);
+            if (bm == 0) {
+                k = (wk + 64) << 6;
+                continue;
+            }
+            const int L = __builtin_ctzll(bm);
+            const unsigned long long wd = ((unsigned long long)rl_u32((uint32_t)(w >> 32), L) << 32) |
+                                          rl_u32((uint32_t)w, L);
+            kb = ((wk + L) << 6) + __builtin_ctzll(wd);
+            if (kb >= nch) break;
         }
-        const unsigned long long m = __ballot(bad);
-        if (m == 0) {
-            k += 64;
-            continue;
-        }
-        const long kb = k + __ffsll((long long)m) - 1;
         // re-run chunk kb from chunk kb-1's end state (lane c handles component c)
         if (lane < ncomp) {
             const int c = lane;
@@ -256,6 +325,7 @@ __global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         k = kb + 1;
+        direct = true;
     }
     // carried state = end state of the last chunk
     for (int i = lane; i < per; i += 64) state[i] = ldnt(sc + ((nch - 1) * 2 + 1) * per + i);
@@ -800,6 +870,16 @@ void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state,
     LDSP_HIP(hipGetLastError());
 }
 
+size_t spec_flags_offset(long nchunks, int ncomp, int fs)
+{
+    return ((size_t)nchunks * 2 * ncomp * fs * sizeof(float) + 255) / 256 * 256;
+}
+
+size_t spec_scratch_bytes(long nchunks, int ncomp, int fs)
+{
+    return spec_flags_offset(nchunks, ncomp, fs) + (size_t)((nchunks + 63) / 64 + 64) * 8;
+}
+
 void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, const SpecPlan& p, void* y,
               hipStream_t s)
 {
@@ -812,10 +892,18 @@ void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state
                            (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks, (float*)p.scratch, (float*)y);
     }
     LDSP_HIP(hipGetLastError());
+    const int fs = d.sos ? 3 * d.nsos : d.nv;
+    unsigned long long* flags = (unsigned long long*)((char*)p.scratch + spec_flags_offset(p.nchunks, ncomp, fs));
+    {
+        LDSP_PROF(s, "k_iir_spec_flags");
+        hipLaunchKernelGGL(k_iir_spec_flags, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, d, ncomp, p.C,
+                           p.W, p.nchunks, (const float*)p.scratch, flags);
+    }
+    LDSP_HIP(hipGetLastError());
     {
         LDSP_PROF(s, "k_iir_spec_verify");
         hipLaunchKernelGGL(k_iir_spec_verify, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, ncomp, p.C, p.W,
-                           p.nchunks, (float*)p.scratch, state, (float*)y);
+                           p.nchunks, (float*)p.scratch, (const unsigned long long*)flags, state, (float*)y);
     }
     LDSP_HIP(hipGetLastError());
 }

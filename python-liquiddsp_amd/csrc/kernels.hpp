@@ -112,6 +112,9 @@ struct SpecPlan {
     long nchunks;
     void* scratch;        // device scratch (states: start-guess and end per chunk)
 };
+// scratch for iir_spec: chunk states + verifier flag words
+size_t spec_flags_offset(long nchunks, int ncomp, int fs);
+size_t spec_scratch_bytes(long nchunks, int ncomp, int fs);
 void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, const SpecPlan& p, void* y,
               hipStream_t s);
 
@@ -124,6 +127,7 @@ struct AgcState {         // device-resident agc_crcf state
     int pad[3];
 };
 void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hipStream_t s);
+size_t agc_scratch_bytes(long nchunks);
 void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
               hipStream_t s);
 
