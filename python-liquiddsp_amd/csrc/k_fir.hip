@@ -324,12 +324,79 @@ __global__ void __launch_bounds__(64) k_resamp(const void* __restrict__ xv_, con
     }
 }
 
+// Direct variant (used when the branch table fits in LDS): one output per
+// thread, its sub_len window read straight from global memory.  Neighbouring
+// outputs' windows are ~1/rate samples apart, so a wave's loads touch ~64 lines
+// per instruction but every line is fetched from HBM once and re-read from L1;
+// no LDS staging or workgroup barrier sits between the loads and the math.
+template <bool CPLX>
+__global__ void __launch_bounds__(256) k_resamp_direct(const void* __restrict__ xv_, const void* __restrict__ hist_,
+                                                       void* __restrict__ hist_out_, long n,
+                                                       const float* __restrict__ sub, ResampPlan p,
+                                                       void* __restrict__ y_)
+{
+    using T = typename std::conditional<CPLX, float2, float>::type;
+    const T* __restrict__ x = (const T*)xv_;
+    const T* __restrict__ hist = (const T*)hist_;
+    T* hist_out = (T*)hist_out_;
+    T* y = (T*)y_;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* taps = reinterpret_cast<T*>(smem);                  // [npfb][sub_len]
+    const int tid = threadIdx.x;
+    const int halo = p.sub_len - 1;
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < halo; j += 256) {
+            const long gi = n - halo + j;
+            hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+        }
+    }
+    const T* subT = (const T*)sub;
+    for (int i = tid; i < p.npfb * p.sub_len; i += 256) taps[i] = subT[i];
+    __syncthreads();
+    const long k = (long)blockIdx.x * 256 + tid;
+    if (k >= (long)p.K) return;
+    const long j = resamp_j(p.P0, k, p.step);
+    const uint64_t ph = p.P0 + (uint64_t)k * p.step - ((uint64_t)j << 24);
+    const int b = (int)(ph >> p.bits_index);
+    const T* hb = taps + (size_t)b * p.sub_len;
+    const long g0 = j - halo;
+    T r{};
+    if (g0 >= 0) {
+        const T* xb = x + g0;
+        for (int i = 0; i < p.sub_len; i++) {
+            if constexpr (CPLX) rs_mac(r, hb[i], xb[i]);
+            else r = r + hb[i] * xb[i];
+        }
+    } else {
+        for (int i = 0; i < p.sub_len; i++) {
+            const long gi = g0 + i;
+            const T v = gi >= 0 ? x[gi] : hist[gi + halo];
+            if constexpr (CPLX) rs_mac(r, hb[i], v);
+            else r = r + hb[i] * v;
+        }
+    }
+    y[k] = r;
+}
+
 } // namespace
 
 void resamp(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
             const ResampPlan& p, void* y, hipStream_t s)
 {
     const size_t elem = cplx ? 8 : 4;
+    const size_t tap_lds = (size_t)p.npfb * p.sub_len * elem;
+    if (tap_lds <= 32 * 1024 && p.K > 0) {
+        const unsigned g = (unsigned)((p.K + 255) / 256);
+        LDSP_PROF(s, "k_resamp");
+        if (cplx)
+            hipLaunchKernelGGL(k_resamp_direct<true>, dim3(g), dim3(256), tap_lds, s, x, hist, hist_out, (long)n, sub,
+                               p, y);
+        else
+            hipLaunchKernelGGL(k_resamp_direct<false>, dim3(g), dim3(256), tap_lds, s, x, hist, hist_out, (long)n,
+                               sub, p, y);
+        LDSP_HIP(hipGetLastError());
+        return;
+    }
     const size_t lds = (size_t)p.span_max * elem;
     const unsigned grid = (unsigned)std::max<size_t>(1, (p.K + p.KB - 1) / p.KB);
     if (cplx) {
