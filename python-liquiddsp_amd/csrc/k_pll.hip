@@ -228,16 +228,17 @@ struct LoadRegs {
     uint32_t w;
 };
 
+// Unconditional (clamped) loads: predicated loads into the same registers made
+// the compiler serialise them with a vmcnt wait each, i.e. one HBM round trip
+// per slot in every block.
 __device__ __forceinline__ void walk_fetch(LoadRegs& r, const CandBuf& cb, long blk, int lt)
 {
     const uint4* src = cb.rec + blk * kVec;
 #pragma unroll
-    for (int k = 0; k < kLoadSlots; k++) {
-        const int q = lt + k * kLoaders;
-        if (q < kVec) r.v[k] = src[q];
-    }
-    r.w = lt < 2 * kSub ? cb.cs[blk * 2 * kSub + lt]
-                        : (lt < 4 * kSub ? cb.ce[blk * 2 * kSub + lt - 2 * kSub] : 0u);
+    for (int k = 0; k < kLoadSlots; k++) r.v[k] = src[min(lt + k * kLoaders, kVec - 1)];
+    const int wi = min(lt, 4 * kSub - 1);
+    const uint32_t* wsrc = wi < 2 * kSub ? cb.cs + blk * 2 * kSub + wi : cb.ce + blk * 2 * kSub + wi - 2 * kSub;
+    r.w = *wsrc;
 }
 
 __device__ __forceinline__ void walk_store(WalkBuf& b, const LoadRegs& r, int lt)
@@ -249,6 +250,55 @@ __device__ __forceinline__ void walk_store(WalkBuf& b, const LoadRegs& r, int lt
     }
     if (lt < 2 * kSub) b.cs[lt] = r.w;
     else if (lt < 4 * kSub) b.ce[lt - 2 * kSub] = r.w;
+}
+
+// LDS-DMA record streaming (global_load_lds_dwordx4: each lane's 16 B land at
+// M0 + 16 lane, no VGPR staging, no compiler-inserted waits).  Loader wave w
+// (0..6) moves the 1 KiB pieces w, w + 7, ... of a block's 32 KiB of records;
+// wave 0 also moves the 2 x 8 chunk-state words.  Every loader wave issues
+// the same number of DMAs per block (kDmaPer, padding with a repeat of its
+// last piece), so one immediate s_waitcnt vmcnt covers the two blocks still
+// in flight.
+constexpr int kPieces = kBlk * 2 * 16 / 1024;              // 32
+constexpr int kLoadWaves = kWalkThreads / 64 - 1;          // 7
+constexpr int kDmaPer = (kPieces + kLoadWaves - 1) / kLoadWaves + 2;   // 5 pieces + 2 state DMAs
+static_assert(kDmaPer == 7, "walker DMA wait count below assumes 7 DMAs per loader wave per block");
+
+// M0 is compiler-reserved: save / set / restore it inside one statement
+// (cdna_hip_programming.md LDS-DMA recipe); asm loads are invisible to hipcc's
+// waitcnt bookkeeping, the walker counts them itself (s_waitcnt vmcnt(N)).
+__device__ __forceinline__ void dma16(uint32_t lds_byte, const void* g)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds_byte)
+                 : "memory");
+}
+__device__ __forceinline__ void dma4(uint32_t lds_byte, const void* g)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds_byte)
+                 : "memory");
+}
+
+__device__ __forceinline__ void walk_dma(WalkBuf& b, const CandBuf& cb, long blk, int lw, int lane)
+{
+    const char* src = (const char*)(cb.rec + blk * kVec);
+    const uint32_t base = (uint32_t)(uintptr_t)&b.rec[0];
+#pragma unroll
+    for (int t = 0; t < kDmaPer - 2; t++) {
+        const int piece = min(lw + t * kLoadWaves, kPieces - 1);        // a repeat is harmless
+        dma16(base + piece * 1024, src + piece * 1024 + lane * 16);
+    }
+    // chunk states: 8 cs words, 8 ce words (lanes 0..7; the instruction still counts once in vmcnt)
+    const int wl = lane & 7;
+    if (lane < 8) {
+        dma4((uint32_t)(uintptr_t)&b.cs[0], cb.cs + blk * 2 * kSub + wl);
+        dma4((uint32_t)(uintptr_t)&b.ce[0], cb.ce + blk * 2 * kSub + wl);
+    }
 }
 
 // Inputs of the rare full step (true index more than one cell from the candidate's).
@@ -400,7 +450,12 @@ __device__ __forceinline__ void walk_sub3(const uint4 (&D)[4][2], int base0, int
                 dk2 = __builtin_amdgcn_readfirstlane(f.y);
                 ob = __builtin_amdgcn_readfirstlane(f.z);
             }
-            asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(pout) : "s"(ob), "s"(j) : "m0");
+            {
+                unsigned keep;    // M0 is compiler-reserved: save and restore it in the same statement
+                asm volatile("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
+                             : "+v"(pout), "=&s"(keep)
+                             : "s"(ob), "s"(j));
+            }
             PM |= 1ull << j;
             K += dk2 - (uint32_t)j * dk1;
             DD += dk1;
@@ -422,18 +477,21 @@ template <bool F24>
 __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, long nblk, CandBuf cb,
                                                            float* __restrict__ y)
 {
-    __shared__ WalkBuf buf[2];
+    __shared__ WalkBuf buf[4];           // ring: block c in buf[c & 3], DMA'd three blocks ahead
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: keeps the walk on SALU
     const int lane = tid & 63;
-    const int lt = tid - 64;
-    LoadRegs lr;
+    const int lw = wave - 1;             // loader wave index 0..6
     if (wave != 0) {
-        walk_fetch(lr, cb, 0, lt);
-        walk_store(buf[0], lr, lt);
-        if (nblk > 1) walk_fetch(lr, cb, 1, lt);
+        for (long b0 = 0; b0 < 3 && b0 < nblk; b0++) walk_dma(buf[b0], cb, b0, lw, lane);
+        // block 0 landed: at most the DMAs of blocks 1 and 2 still in flight
+        if (nblk > 2) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        else if (nblk > 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     FullCtx fc;
     fc.x0 = in.x0;
     fc.x = in.x;
@@ -450,12 +508,14 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     for (long c = 0; c < nblk; c++) {
         const unsigned long long t0 = wall_clock64();
         if (wave != 0) {
-            if (c + 1 < nblk) {
-                walk_store(buf[(c + 1) & 1], lr, lt);
-                if (c + 2 < nblk) walk_fetch(lr, cb, c + 2, lt);
-            }
+            // slot (c + 3) & 3 held block c - 1, released by the previous barrier
+            if (c + 3 < nblk) walk_dma(buf[(c + 3) & 3], cb, c + 3, lw, lane);
+            // block c + 1 must have landed before the barrier below publishes it
+            if (c + 3 < nblk) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+            else if (c + 2 < nblk) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
-            const WalkBuf& b = buf[c & 1];
+            const WalkBuf& b = buf[c & 3];
             const long s0 = c * kBlk;
             const int cnt = (int)min((long)kBlk, n - s0);
             float* yb = y + s0;
