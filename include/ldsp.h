@@ -103,8 +103,14 @@ int ldsp_firfilt_execute(ldsp_firfilt_t q, const void *x, size_t n, void *y, int
  * resamp_*_execute per sample, set_rate, reset, print).
  * ---------------------------------------------------------------------- */
 typedef struct ldsp_resamp_s *ldsp_resamp_t;
+/* cplx: 0 resamp_rrrf, 1 resamp_cccf (ComplexResampler), 2 resamp_crcf (complex
+ * samples, real taps: CResampler) */
 int ldsp_resamp_create(float rate, unsigned int m, float fc, float as, unsigned int npfb, int cplx,
                        ldsp_resamp_t *q);
+/* resamp_*_create_default(rate): RResampler / CResampler (src/resampler.hpp:10-13,
+ * 46-49; wrapper.cpp:15-23).  m = 7, fc = 0.25, As = 60, npfb = 256 (liquid-dsp
+ * resamp.proto.c defaults, recalled: parity unpinned). */
+int ldsp_resamp_create_default(float rate, int kind, ldsp_resamp_t *q);
 int ldsp_resamp_destroy(ldsp_resamp_t q);
 int ldsp_resamp_reset(ldsp_resamp_t q);
 int ldsp_resamp_set_rate(ldsp_resamp_t q, float rate);
@@ -210,6 +216,54 @@ int ldsp_ampmodem_reset(ldsp_ampmodem_t q);
 int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t *theta, uint32_t *dtheta);
 int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void *x, size_t n, void *y, int mem,
                              void *stream);
+
+/* ------------------------------------------------------------------------
+ * Broadcast AM demodulator.  Replaces BroadcastAM (src/demod.hpp:93-153,
+ * wrapper.cpp:259-262): carrier PLL (Kaiser lowpass 2m+1, wdelaycf(m), NCO
+ * PLL bw 0.001) followed by a cheby2 SOS highpass DC blocker (order 3,
+ * fc 20/48000, Ap 0.5, As 20).  The PLL stage is bit-exact; the DC blocker
+ * runs in LDSP_MODE_FAST (fp64 scan) by default, LDSP_MODE_EXACT on request.
+ * `pre` (optional, device-or-host like y) receives re(v1) before the blocker.
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_bcastam_s *ldsp_bcastam_t;
+int ldsp_bcastam_create(unsigned int m, ldsp_bcastam_t *q);
+int ldsp_bcastam_destroy(ldsp_bcastam_t q);
+int ldsp_bcastam_reset(ldsp_bcastam_t q);
+int ldsp_bcastam_set_mode(ldsp_bcastam_t q, int mode);
+int ldsp_bcastam_get_mode(ldsp_bcastam_t q, int *mode);
+int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void *x, size_t n, void *y, void *pre, int mem,
+                            void *stream);
+
+/* ------------------------------------------------------------------------
+ * Frequency demodulator.  Replaces FreqDem (src/demod.hpp:189-219,
+ * wrapper.cpp:183-187 -> freqdem_create(kf), freqdem_demodulate_block):
+ * y[n] = cargf(conjf(x[n-1]) x[n]) / (2 pi kf), bit-exact.
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_freqdem_s *ldsp_freqdem_t;
+int ldsp_freqdem_create(float kf, ldsp_freqdem_t *q);
+int ldsp_freqdem_destroy(ldsp_freqdem_t q);
+int ldsp_freqdem_reset(ldsp_freqdem_t q);
+int ldsp_freqdem_get_kf(ldsp_freqdem_t q, float *kf);
+int ldsp_freqdem_demodulate(ldsp_freqdem_t q, const void *x, size_t n, void *y, int mem, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Sample delay line.  Replaces Delay (src/utility.hpp:5-57, wrapper.cpp:25-28):
+ * separate real (wdelayf) and complex (wdelaycf) lines of nd, read-then-push,
+ * i.e. y[n] = x[n - nd - 1].  set_delay re-creates (zeroes) both lines.
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_delay_s *ldsp_delay_t;
+int ldsp_delay_create(unsigned int nd, ldsp_delay_t *q);
+int ldsp_delay_destroy(ldsp_delay_t q);
+int ldsp_delay_set_delay(ldsp_delay_t q, unsigned int nd);
+int ldsp_delay_get_delay(ldsp_delay_t q, unsigned int *nd);
+int ldsp_delay_execute(ldsp_delay_t q, const void *x, size_t n, int cplx, void *y, int mem, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Raw IQ conversion.  Replaces bytes_to_iq (src/utility.hpp:61-69,
+ * wrapper.cpp:13): interleaved native int16 (I, Q) -> complex64 / 32767.
+ * nbytes / 4 samples are converted (a trailing partial sample is ignored).
+ * ---------------------------------------------------------------------- */
+int ldsp_bytes_to_iq(const void *in, size_t nbytes, void *y, int mem, void *stream);
 
 #ifdef __cplusplus
 }

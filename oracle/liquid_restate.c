@@ -357,7 +357,7 @@ void ora_firfilt_execute_block(ora_firfilt q, const float *x, size_t n, float *y
 /* reference: src/resampler.hpp:72-173 (resamp_rrrf / resamp_cccf)        */
 /* ===================================================================== */
 struct ora_resamp_s {
-    int kind;                 /* 0 rrrf, 2 cccf */
+    int kind;                 /* 0 rrrf, 1 crcf, 2 cccf */
     unsigned int m, npfb, bits_index, sub_len;
     float fc, as, rate;
     uint32_t step, phase;
@@ -425,6 +425,13 @@ ora_resamp ora_resamp_create(float rate, unsigned int m, float fc, float as,
     return q;
 }
 
+/* resamp_*_create_default (liquid resamp.proto.c, recalled): m = 7, fc = 0.25,
+ * As = 60, npfb = 256.  Reference: RResampler / CResampler, src/resampler.hpp:10-13,46-49. */
+ora_resamp ora_resamp_create_default(float rate, int kind)
+{
+    return ora_resamp_create(rate, 7, 0.25f, 60.0f, 256, kind);
+}
+
 void ora_resamp_destroy(ora_resamp q)
 {
     if (!q) return;
@@ -457,6 +464,8 @@ size_t ora_resamp_execute_block(ora_resamp q, const float *x, size_t n, float *y
             unsigned int index = q->phase >> q->bits_index;
             if (q->kind == 0) {
                 y[nw] = dot_rr(q->sub + (size_t)index * q->sub_len, r, q->sub_len);
+            } else if (q->kind == 1) {
+                dot_cr(q->sub + (size_t)index * q->sub_len, r, q->sub_len, y + 2 * nw);
             } else {
                 dot_cc(q->sub + (size_t)index * q->sub_len * 2, r, q->sub_len, y + 2 * nw);
             }
@@ -1440,4 +1449,105 @@ size_t ora_amradio_execute(ora_amradio q, const float *x, size_t n, float *y)
     ora_ampmodem_demodulate_block(q->am, q->buf2, nr, q->buf0);
     ora_iirfilt_execute_block(q->deemph, q->buf0, nr, y);
     return nr;
+}
+
+/* ===================================================================== */
+/* freqdem: liquid src/modem/src/freqdem.c (liquid >= 1.3)              */
+/* reference: FreqDem src/demod.hpp:189-219, wrapper.cpp:183-187          */
+/*   ref = 1 / (2 pi kf);  m[n] = cargf(conjf(r[n-1]) * r[n]) * ref      */
+/* ===================================================================== */
+struct ora_freqdem_s {
+    float kf, ref;
+    float rp[2];
+};
+ora_freqdem ora_freqdem_create(float kf)
+{
+    ora_freqdem q = (ora_freqdem)calloc(1, sizeof(*q));
+    q->kf = kf;
+    q->ref = 1.0f / (2 * M_PI * q->kf);
+    return q;
+}
+void ora_freqdem_destroy(ora_freqdem q) { free(q); }
+void ora_freqdem_reset(ora_freqdem q) { q->rp[0] = q->rp[1] = 0.0f; }
+void ora_freqdem_demodulate_block(ora_freqdem q, const float *x, size_t n, float *y)
+{
+    size_t i;
+    for (i = 0; i < n; i++) {
+        /* conjf(r') * r with C99 float complex multiply: (a + jb')(c + jd), b' = -b */
+        const float a = q->rp[0], bq = -q->rp[1], c = x[2 * i], d = x[2 * i + 1];
+        const float re = a * c - bq * d;
+        const float im = a * d + bq * c;
+        y[i] = om_atan2f(im, re) * q->ref;
+        q->rp[0] = c;
+        q->rp[1] = d;
+    }
+}
+
+/* ===================================================================== */
+/* BroadcastAM: reference src/demod.hpp:93-153 (python-liquiddsp's own   */
+/* demodulator): Kaiser lowpass 2m+1 (fc 0.01, As 40) + wdelaycf(m) +    */
+/* NCO PLL (bw 0.001) on cargf(v0), output through an SOS cheby2         */
+/* highpass DC blocker (order 3, fc 20/48000, Ap 0.5, As 20) on re(v1).   */
+/* ===================================================================== */
+struct ora_bcastam_s {
+    unsigned int m;
+    ora_nco mixer;
+    ora_firfilt lowpass;
+    ora_iirfilt dcblock;
+    float *delay;
+    unsigned int dpos;
+};
+ora_bcastam ora_bcastam_create(unsigned int m, int iir_f64)
+{
+    ora_bcastam q = (ora_bcastam)calloc(1, sizeof(*q));
+    q->m = m;
+    q->mixer = ora_nco_create(0);
+    ora_nco_pll_set_bandwidth(q->mixer, 0.001f);
+    q->lowpass = ora_firfilt_create_kaiser(2 * m + 1, 0.01f, 40.0f, 0.0f, 1);
+    q->dcblock = ora_iirfilt_create_prototype(2, 1, 1, 3, 20.0f / 48000.0f, 0.0f, 0.5f, 20.0f, 0);
+    (void)iir_f64;
+    q->delay = (float *)calloc(2 * (m + 1), sizeof(float));
+    return q;
+}
+void ora_bcastam_destroy(ora_bcastam q)
+{
+    if (!q) return;
+    ora_nco_destroy(q->mixer);
+    ora_firfilt_destroy(q->lowpass);
+    ora_iirfilt_destroy(q->dcblock);
+    free(q->delay);
+    free(q);
+}
+void ora_bcastam_reset(ora_bcastam q)
+{
+    ora_nco_reset(q->mixer);
+    ora_firfilt_reset(q->lowpass);
+    ora_iirfilt_reset(q->dcblock);
+    memset(q->delay, 0, 2 * (q->m + 1) * sizeof(float));
+    q->dpos = 0;
+}
+/* y: the PLL output re(v1) before the DC blocker (pre) and after it (y) */
+void ora_bcastam_demodulate_block(ora_bcastam q, const float *x, size_t n, float *pre, float *y, int iir_f64)
+{
+    size_t i;
+    for (i = 0; i < n; i++) {
+        float x0[2], x1[2], v0r, v0i, v1r, v1i, s, c;
+        firfilt_push_exec(q->lowpass, x + 2 * i, x0);
+        /* wdelaycf push then read: the sample pushed m samples earlier */
+        unsigned int len = q->m + 1;
+        q->delay[2 * q->dpos] = x[2 * i];
+        q->delay[2 * q->dpos + 1] = x[2 * i + 1];
+        q->dpos = (q->dpos + 1) % len;
+        x1[0] = q->delay[2 * q->dpos];
+        x1[1] = q->delay[2 * q->dpos + 1];
+        nco_sincos(q->mixer, &s, &c);
+        cmul_down(x0[0], x0[1], c, s, &v0r, &v0i);
+        cmul_down(x1[0], x1[1], c, s, &v1r, &v1i);
+        float phase_error = om_atan2f(v0i, v0r);
+        ora_nco_pll_step(q->mixer, phase_error);
+        q->mixer->theta += q->mixer->d_theta;
+        pre[i] = v1r;
+    }
+    if (iir_f64) ora_iirfilt_execute_block_f64(q->dcblock, pre, n, y);
+    else ora_iirfilt_execute_block(q->dcblock, pre, n, y);
 }

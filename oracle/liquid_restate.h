@@ -45,6 +45,7 @@ void  ora_firfilt_execute_block(ora_firfilt q, const float *x, size_t n, float *
 
 /* ---- resamp (rrrf: kind 0, cccf: kind 2) ------------------------------ */
 typedef struct ora_resamp_s *ora_resamp;
+ora_resamp ora_resamp_create_default(float rate, int kind);   /* kind: 0 rrrf, 1 crcf, 2 cccf */
 ora_resamp ora_resamp_create(float rate, unsigned int m, float fc, float as,
                              unsigned int npfb, int kind);
 void     ora_resamp_destroy(ora_resamp q);
@@ -141,6 +142,18 @@ ora_amradio ora_amradio_create(float bandwidth, float iq_rate, float pcm_rate, i
 void   ora_amradio_destroy(ora_amradio q);
 size_t ora_amradio_max_out(ora_amradio q, size_t n);
 size_t ora_amradio_execute(ora_amradio q, const float *x, size_t n, float *y);
+
+/* ---- freqdem, BroadcastAM ------------------------------------------- */
+typedef struct ora_freqdem_s *ora_freqdem;
+ora_freqdem ora_freqdem_create(float kf);
+void ora_freqdem_destroy(ora_freqdem q);
+void ora_freqdem_reset(ora_freqdem q);
+void ora_freqdem_demodulate_block(ora_freqdem q, const float *x, size_t n, float *y);
+typedef struct ora_bcastam_s *ora_bcastam;
+ora_bcastam ora_bcastam_create(unsigned int m, int iir_f64);
+void ora_bcastam_destroy(ora_bcastam q);
+void ora_bcastam_reset(ora_bcastam q);
+void ora_bcastam_demodulate_block(ora_bcastam q, const float *x, size_t n, float *pre, float *y, int iir_f64);
 
 #ifdef __cplusplus
 }

@@ -57,6 +57,15 @@ def _load():
         "ora_firfilt_freqresponse": (None, [vp, f, C.POINTER(f), C.POINTER(f)]),
         "ora_firfilt_execute_block": (None, [vp, f32p, sz, f32p]),
         "ora_resamp_create": (vp, [f, u, f, f, u, i]),
+        "ora_resamp_create_default": (vp, [f, i]),
+        "ora_freqdem_create": (vp, [f]),
+        "ora_freqdem_destroy": (None, [vp]),
+        "ora_freqdem_reset": (None, [vp]),
+        "ora_freqdem_demodulate_block": (None, [vp, f32p, sz, f32p]),
+        "ora_bcastam_create": (vp, [u, i]),
+        "ora_bcastam_destroy": (None, [vp]),
+        "ora_bcastam_reset": (None, [vp]),
+        "ora_bcastam_demodulate_block": (None, [vp, f32p, sz, f32p, f32p, i]),
         "ora_resamp_destroy": (None, [vp]),
         "ora_resamp_reset": (None, [vp]),
         "ora_resamp_set_rate": (i, [vp, f]),
@@ -242,12 +251,17 @@ class FIRFilter(_Handle):
 
 
 class Resampler(_Handle):
-    """resamp_rrrf (cplx=False) / resamp_cccf (cplx=True)."""
+    """resamp_rrrf (cplx=False) / resamp_cccf (cplx=True) / resamp_crcf
+    (cplx=True, real_taps=True); default=True: resamp_*_create_default(rate)."""
     _destroy = "ora_resamp_destroy"
 
-    def __init__(self, rate, m=20, fc=0.25, As=60.0, npfb=13, cplx=True):
+    def __init__(self, rate, m=20, fc=0.25, As=60.0, npfb=13, cplx=True, real_taps=False, default=False):
         self.cplx = bool(cplx)
-        self._h = lib().ora_resamp_create(rate, m, fc, As, npfb, 2 if cplx else 0)
+        kind = (1 if real_taps else 2) if cplx else 0
+        if default:
+            self._h = lib().ora_resamp_create_default(rate, kind)
+        else:
+            self._h = lib().ora_resamp_create(rate, m, fc, As, npfb, kind)
         if not self._h:
             raise ValueError("resamp: invalid configuration")
 
@@ -524,3 +538,75 @@ class AMRadio(_Handle):
         y = np.empty(lib().ora_amradio_max_out(self._h, n), np.float32)
         nw = lib().ora_amradio_execute(self._h, xf, n, y)
         return y[:nw].copy()
+
+
+class FreqDem(_Handle):
+    """freqdem (FreqDem, src/demod.hpp:189-219): m = cargf(conj(r[n-1]) r[n]) / (2 pi kf)."""
+    _destroy = "ora_freqdem_destroy"
+
+    def __init__(self, kf):
+        self._h = lib().ora_freqdem_create(kf)
+
+    def reset(self):
+        lib().ora_freqdem_reset(self._h)
+
+    def __call__(self, x):
+        xf = _c64_as_f32(x)
+        y = np.empty(len(x), np.float32)
+        lib().ora_freqdem_demodulate_block(self._h, xf, len(x), y)
+        return y
+
+
+class BroadcastAM(_Handle):
+    """BroadcastAM (src/demod.hpp:93-153).  iir_f64: evaluate the DC-blocking
+    IIR in float64 (the reference for the GPU's fast IIR mode)."""
+    _destroy = "ora_bcastam_destroy"
+
+    def __init__(self, slen=25, iir_f64=False):
+        self.iir_f64 = int(iir_f64)
+        self._h = lib().ora_bcastam_create(slen, self.iir_f64)
+
+    def reset(self):
+        lib().ora_bcastam_reset(self._h)
+
+    def __call__(self, x, return_pre=False):
+        xf = _c64_as_f32(x)
+        pre = np.empty(len(x), np.float32)
+        y = np.empty(len(x), np.float32)
+        lib().ora_bcastam_demodulate_block(self._h, xf, len(x), pre, y, self.iir_f64)
+        return (pre, y) if return_pre else y
+
+
+class Delay:
+    """wdelay read-then-push (Delay, src/utility.hpp:5-57): liquid's wdelay of
+    `nd` holds nd + 1 samples, so y[n] = x[n - nd - 1] (zero history).  Real
+    and complex streams keep separate lines, as in the reference."""
+
+    def __init__(self, nd=1):
+        self.delay = nd
+
+    @property
+    def delay(self):
+        return self._nd
+
+    @delay.setter
+    def delay(self, nd):
+        self._nd = int(nd)
+        self._hist = {np.dtype(np.complex64): np.zeros(self._nd + 1, np.complex64),
+                      np.dtype(np.float32): np.zeros(self._nd + 1, np.float32)}
+
+    def __call__(self, x):
+        x = np.asarray(x)
+        if x.dtype not in self._hist:
+            return None
+        buf = np.concatenate([self._hist[x.dtype], x])
+        self._hist[x.dtype] = buf[len(buf) - (self._nd + 1):].copy()
+        return buf[:len(x)].copy()
+
+
+def bytes_to_iq(b):
+    """bytes_to_iq (src/utility.hpp:61-69): int16 (I, Q) pairs / 32767.0f."""
+    b = bytes(b)
+    a = np.frombuffer(b[: (len(b) // 4) * 4], dtype=np.int16).astype(np.float32)
+    y = (a / np.float32(32767.0)).astype(np.float32)
+    return y.view(np.complex64)

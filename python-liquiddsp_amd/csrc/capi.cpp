@@ -73,6 +73,15 @@ static T* upload(DevBuf& b, const std::vector<T>& v, int dev)
     return b.as<T>();
 }
 
+// Zero device memory before any stream can read it: hipMemset runs on the
+// null stream, which does not order against the non-blocking library stream or
+// a caller's stream, so wait for it (create / reset paths only).
+static void zero_now(void* p, int v, size_t bytes)
+{
+    LDSP_HIP(hipMemset(p, v, bytes));
+    LDSP_HIP(hipDeviceSynchronize());
+}
+
 // Host <-> device staging for LDSP_MEM_HOST calls
 struct Staging {
     DevBuf in, out;
@@ -166,7 +175,7 @@ struct FirObj {
         upload(taps_rev, rev, dev);
         for (auto& b : hist) {
             b.ensure(std::max<size_t>(L - 1, 1) * esz(), dev);
-            LDSP_HIP(hipMemset(b.p, 0, std::max<size_t>(L - 1, 1) * esz()));
+            zero_now(b.p, 0, std::max<size_t>(L - 1, 1) * esz());
         }
         device = dev;
     }
@@ -184,7 +193,8 @@ namespace ldsp {
 
 // ====================================================================== resampler
 struct ResampObj {
-    bool cplx = true;
+    bool cplx = true;                 // complex samples
+    bool real_taps = false;           // crcf: complex samples, real taps (CResampler)
     float rate = 1.0f;
     unsigned int m = 0, npfb = 0, sub_len = 0;
     int bits_index = 0;
@@ -218,7 +228,7 @@ struct ResampObj {
         upload(dsub, sub, dev);
         for (auto& b : hist) {
             b.ensure(std::max<size_t>(sub_len - 1, 1) * esz(), dev);
-            LDSP_HIP(hipMemset(b.p, 0, std::max<size_t>(sub_len - 1, 1) * esz()));
+            zero_now(b.p, 0, std::max<size_t>(sub_len - 1, 1) * esz());
         }
         device = dev;
     }
@@ -362,9 +372,9 @@ struct IirObj {
         upload(db, b, dev);
         upload(da, a, dev);
         st32.ensure(sizeof(float) * 2 * std::max(fsz(), 1), dev);
-        LDSP_HIP(hipMemset(st32.p, 0, sizeof(float) * 2 * std::max(fsz(), 1)));
+        zero_now(st32.p, 0, sizeof(float) * 2 * std::max(fsz(), 1));
         st64.ensure(sizeof(double) * 2 * std::max(D, 1), dev);
-        LDSP_HIP(hipMemset(st64.p, 0, sizeof(double) * 2 * std::max(D, 1)));
+        zero_now(st64.p, 0, sizeof(double) * 2 * std::max(D, 1));
         state_in64 = false;
         device = dev;
     }
@@ -566,11 +576,11 @@ struct AmpObj {
         LDSP_HIP(hipMemcpy(dst.p, &st, sizeof(st), hipMemcpyHostToDevice));
         for (int i = 0; i < 2; i++) {
             lph[i].ensure((2 * m) * 8, dev);
-            LDSP_HIP(hipMemset(lph[i].p, 0, (2 * m) * 8));
+            zero_now(lph[i].p, 0, (2 * m) * 8);
             dch[i].ensure((2 * m) * 4, dev);
-            LDSP_HIP(hipMemset(dch[i].p, 0, (2 * m) * 4));
+            zero_now(dch[i].p, 0, (2 * m) * 4);
             dlh[i].ensure(m * 8, dev);
-            LDSP_HIP(hipMemset(dlh[i].p, 0, m * 8));
+            zero_now(dlh[i].p, 0, m * 8);
         }
         device = dev;
     }
@@ -583,6 +593,38 @@ struct ldsp_nco_s : ldsp::NcoObj {};
 struct ldsp_iirfilt_s : ldsp::IirObj {};
 struct ldsp_agc_s : ldsp::AgcObj {};
 struct ldsp_ampmodem_s : ldsp::AmpObj {};
+
+// BroadcastAM: the AmpModem carrier-PLL stage with mod_index 1 (re(v1) / 1
+// == re(v1)) followed by an owned SOS IIR DC blocker instead of the FIR one.
+struct ldsp_bcastam_s : ldsp::AmpObj {
+    ldsp_iirfilt_t dcb = nullptr;
+};
+
+// Streaming state of the per-sample kernels lives on the device, ping-ponged
+// between two buffers so a call never reads what it writes.
+struct ldsp_freqdem_s {
+    float kf = 0.0f, ref = 0.0f;
+    int device = -1, cur = 0;
+    ldsp::DevBuf prev[2];
+    hipStream_t last = nullptr;
+    ldsp::Staging stg;
+};
+
+struct ldsp_delay_s {
+    unsigned int nd = 1;
+    int device = -1, cr = 0, cc = 0;
+    ldsp::DevBuf hr[2], hc[2];     // real / complex lines of nd + 1 samples
+    hipStream_t last = nullptr;
+    ldsp::Staging stg;
+    void zero()
+    {
+        for (int i = 0; i < 2; i++) {
+            ldsp::zero_now(hr[i].ensure((nd + 1) * 4, device), 0, (nd + 1) * 4);
+            ldsp::zero_now(hc[i].ensure((nd + 1) * 8, device), 0, (nd + 1) * 8);
+        }
+        cr = cc = 0;
+    }
+};
 
 using namespace ldsp;
 
@@ -869,8 +911,10 @@ int ldsp_resamp_create(float rate, unsigned int m, float fc, float as, unsigned 
         LDSP_REQUIRE(fc > 0.0f && fc < 0.5f, "resamp: filter cutoff must be in (0, 0.5)");
         LDSP_REQUIRE(as > 0.0f, "resamp: filter stop-band suppression must be greater than zero");
         LDSP_REQUIRE(npfb > 0, "resamp: number of filters must be greater than zero");
+        LDSP_REQUIRE(cplx >= 0 && cplx <= 2, "resamp: kind must be 0 (rrrf), 1 (cccf) or 2 (crcf)");
         std::unique_ptr<ldsp_resamp_s> o(new ldsp_resamp_s());
         o->cplx = cplx != 0;
+        o->real_taps = cplx == 2;
         o->set_rate(rate);
         o->m = m;
         o->fc = fc;
@@ -888,13 +932,19 @@ int ldsp_resamp_create(float rate, unsigned int m, float fc, float as, unsigned 
         o->hproto.resize(n);
         for (unsigned int i = 0; i < n; i++) o->hproto[i] = hf[i] * gain;
         o->sub_len = (n - 1) / o->npfb;
-        const unsigned c = o->cplx ? 2 : 1;
+        const unsigned c = (o->cplx && !o->real_taps) ? 2 : 1;
         o->sub.assign((size_t)o->npfb * o->sub_len * c, 0.0f);
         for (unsigned int b = 0; b < o->npfb; b++)
             for (unsigned int k = 0; k < o->sub_len; k++)
                 o->sub[((size_t)b * o->sub_len + (o->sub_len - k - 1)) * c] = o->hproto[b + k * o->npfb];
         *q = o.release();
     });
+}
+
+int ldsp_resamp_create_default(float rate, int kind, ldsp_resamp_t* q)
+{
+    // resamp_*_create_default (liquid resamp.proto.c, recalled): m 7, fc 0.25, As 60, npfb 256
+    return ldsp_resamp_create(rate, 7, 0.25f, 60.0f, 256, kind, q);
 }
 
 int ldsp_resamp_destroy(ldsp_resamp_t q)
@@ -975,7 +1025,7 @@ int ldsp_resamp_execute(ldsp_resamp_t q, const void* x, size_t n, void* y, size_
             while (KB > 1 && (size_t)span_for(KB) * q->esz() > 48 * 1024) KB >>= 1;
             p.KB = KB;
             p.span_max = span_for(KB);
-            k::resamp(q->cplx, dx, q->hist[q->cur].p, q->hist[1 - q->cur].p, n, q->dsub.as<float>(), p, dy,
+            k::resamp(q->cplx, q->real_taps, dx, q->hist[q->cur].p, q->hist[1 - q->cur].p, n, q->dsub.as<float>(), p, dy,
                       e.stream);
             if (q->sub_len > 1) q->cur = 1 - q->cur;
             q->phase = (uint64_t)((long long)q->phase + (long long)K * q->step - (long long)n * (1LL << 24));
@@ -1463,21 +1513,24 @@ int ldsp_ampmodem_destroy(ldsp_ampmodem_t q)
         delete q;
     });
 }
+static void amp_reset(AmpObj* q)
+{
+    q->reset_host();
+    q->dev_newer = false;
+    if (q->device < 0) return;
+    DeviceGuard g(q->device);
+    if (q->last) LDSP_HIP(hipStreamSynchronize(q->last));
+    LDSP_HIP(hipMemcpy(q->dst.p, &q->st, sizeof(q->st), hipMemcpyHostToDevice));
+    for (int i = 0; i < 2; i++) {
+        for (DevBuf* b : {&q->lph[i], &q->dch[i], &q->dlh[i]})
+            if (b->p) zero_now(b->p, 0, b->cap);
+    }
+}
 int ldsp_ampmodem_reset(ldsp_ampmodem_t q)
 {
     return guard([&] {
         NONNULL(q);
-        q->reset_host();
-        q->dev_newer = false;
-        if (q->device < 0) return;
-        DeviceGuard g(q->device);
-        if (q->last) LDSP_HIP(hipStreamSynchronize(q->last));
-        LDSP_HIP(hipMemcpy(q->dst.p, &q->st, sizeof(q->st), hipMemcpyHostToDevice));
-        for (int i = 0; i < 2; i++) {
-            LDSP_HIP(hipMemset(q->lph[i].p, 0, q->lph[i].cap));
-            LDSP_HIP(hipMemset(q->dch[i].p, 0, q->dch[i].cap));
-            LDSP_HIP(hipMemset(q->dlh[i].p, 0, q->dlh[i].cap));
-        }
+        amp_reset(q);
     });
 }
 int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
@@ -1495,6 +1548,26 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
     });
 }
 
+// Carrier lowpass + delay + PLL walk of AmpModem / BroadcastAM: writes
+// re(v1) / mod_index (costas 0) or the Costas-loop output (costas 1) to mbuf.
+static void amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, float mod_index, int costas, float* mbuf)
+{
+    const int L = 2 * (int)q->m + 1;
+    void* x0 = q->x0.ensure(n * 8, q->device);
+    k::fir_exact(true, dx, q->lph[q->cur].p, q->lph[1 - q->cur].p, n, q->dlp.as<float>(), L, 1.0f, x0, e.stream);
+    void* pscr = q->pll.ensure(k::pll_scratch_bytes(n), q->device);
+    k::ampmodem_pll(x0, dx, q->dlh[q->cur].p, q->dlh[1 - q->cur].p, (int)q->m, n, q->dst.as<k::AmpState>(),
+                    q->dtab.as<float>(), mod_index, costas, q->st.alpha, mbuf, pscr, e.stream);
+    if (n >= 8192 && std::getenv("LDSP_DEBUG_PLL")) {
+        unsigned long long stt[4];
+        LDSP_HIP(hipMemcpyAsync(stt, (char*)pscr + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
+                                e.stream));
+        LDSP_HIP(hipStreamSynchronize(e.stream));
+        std::fprintf(stderr, "[ldsp pll] n=%zu repairs=%llu unused=%llu walk_clk=%llu wait_clk=%llu\n", n, stt[0],
+                     stt[1], stt[2], stt[3]);
+    }
+}
+
 int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
     return guard([&] {
@@ -1507,21 +1580,8 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
         if (n > 0) {
             const int L = 2 * (int)q->m + 1;
-            void* x0 = q->x0.ensure(n * 8, q->device);
-            k::fir_exact(true, dx, q->lph[q->cur].p, q->lph[1 - q->cur].p, n, q->dlp.as<float>(), L, 1.0f, x0,
-                         e.stream);
             float* mbuf = q->suppressed ? dy : (float*)q->mb.ensure(n * 4, q->device);
-            void* pscr = q->pll.ensure(k::pll_scratch_bytes(n), q->device);
-            k::ampmodem_pll(x0, dx, q->dlh[q->cur].p, q->dlh[1 - q->cur].p, (int)q->m, n, q->dst.as<k::AmpState>(),
-                            q->dtab.as<float>(), q->mod_index, q->suppressed ? 1 : 0, q->st.alpha, mbuf, pscr, e.stream);
-            if (n >= 8192 && std::getenv("LDSP_DEBUG_PLL")) {
-                unsigned long long stt[4];
-                LDSP_HIP(hipMemcpyAsync(stt, (char*)pscr + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
-                                        e.stream));
-                LDSP_HIP(hipStreamSynchronize(e.stream));
-                std::fprintf(stderr, "[ldsp pll] n=%zu repairs=%llu unused=%llu walk_clk=%llu wait_clk=%llu\n", n, stt[0],
-                             stt[1], stt[2], stt[3]);
-            }
+            amp_pll_stage(q, e, dx, n, q->mod_index, q->suppressed ? 1 : 0, mbuf);
             if (!q->suppressed)
                 k::fir_exact(false, mbuf, q->dch[q->cur].p, q->dch[1 - q->cur].p, n, q->ddc.as<float>(), L, 1.0f,
                              dy, e.stream);
@@ -1530,6 +1590,234 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
         }
         q->last = e.stream;
         q->stg.finish(e, y, n * 4);
+    });
+}
+
+// ---------------------------------------------------------------- BroadcastAM
+int ldsp_bcastam_create(unsigned int m, ldsp_bcastam_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(m >= 1 && m <= 4096, "bcastam: m must be in [1, 4096]");
+        std::unique_ptr<ldsp_bcastam_s> o(new ldsp_bcastam_s());
+        o->mod_index = 1.0f;
+        o->type = 0;
+        o->suppressed = 0;
+        o->m = m;
+        o->lp = design::firdes_kaiser(2 * m + 1, 0.01f, 40.0f, 0.0f);
+        o->table = nco_table();
+        o->reset_host();
+        // cheby2 highpass, SOS, order 3, fc 20/48000, f0 0, Ap 0.5, As 20 (demod.hpp:104)
+        int rc = ldsp_iirfilt_create_prototype(2, 1, 3, 20.0f / 48000.0f, 0.0f, 0.5f, 20.0f, 0, &o->dcb);
+        if (rc != LDSP_OK) throw Error(rc, g_last_error);
+        *q = o.release();
+    });
+}
+int ldsp_bcastam_destroy(ldsp_bcastam_t q)
+{
+    return guard([&] {
+        if (!q) return;
+        if (q->last) (void)hipStreamSynchronize(q->last);
+        ldsp_iirfilt_destroy(q->dcb);
+        delete q;
+    });
+}
+int ldsp_bcastam_reset(ldsp_bcastam_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        amp_reset(q);
+        const int rc = ldsp_iirfilt_reset(q->dcb);
+        if (rc != LDSP_OK) throw Error(rc, g_last_error);
+    });
+}
+int ldsp_bcastam_set_mode(ldsp_bcastam_t q, int mode)
+{
+    return guard([&] {
+        NONNULL(q);
+        const int rc = ldsp_iirfilt_set_mode(q->dcb, mode);
+        if (rc != LDSP_OK) throw Error(rc, g_last_error);
+    });
+}
+int ldsp_bcastam_get_mode(ldsp_bcastam_t q, int* mode)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(mode);
+        *mode = q->dcb->mode;
+    });
+}
+int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void* x, size_t n, void* y, void* pre, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "bcastam_demodulate: NULL buffer");
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const void* dx = q->stg.dev_in(e, x, n * 8);
+        float* dy = (float*)q->stg.dev_out(e, y, n * 4);
+        if (n > 0) {
+            float* mbuf = (float*)q->mb.ensure(n * 4, q->device);
+            amp_pll_stage(q, e, dx, n, 1.0f, 0, mbuf);
+            const int rc = ldsp_iirfilt_execute(q->dcb, mbuf, n, dy, LDSP_MEM_DEVICE, e.stream);
+            if (rc != LDSP_OK) throw Error(rc, g_last_error);
+            if (pre) {
+                LDSP_HIP(hipMemcpyAsync(pre, mbuf, n * 4, e.host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice,
+                                        e.stream));
+            }
+            q->cur = 1 - q->cur;
+            q->dev_newer = true;
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, n * 4);
+    });
+}
+
+// ---------------------------------------------------------------- FreqDem
+int ldsp_freqdem_create(float kf, ldsp_freqdem_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(kf > 0.0f, "freqdem: kf must be > 0");
+        std::unique_ptr<ldsp_freqdem_s> o(new ldsp_freqdem_s());
+        o->kf = kf;
+        o->ref = (float)(1.0 / (2 * M_PI * (double)kf));   // freqdem.c: 1/(2*M_PI*kf) in double, stored float
+        *q = o.release();
+    });
+}
+int ldsp_freqdem_destroy(ldsp_freqdem_t q)
+{
+    return guard([&] {
+        if (q && q->last) (void)hipStreamSynchronize(q->last);
+        delete q;
+    });
+}
+int ldsp_freqdem_reset(ldsp_freqdem_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (q->device < 0) return;
+        DeviceGuard g(q->device);
+        if (q->last) LDSP_HIP(hipStreamSynchronize(q->last));
+        for (int i = 0; i < 2; i++) zero_now(q->prev[i].p, 0, 8);
+    });
+}
+int ldsp_freqdem_get_kf(ldsp_freqdem_t q, float* kf)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(kf);
+        *kf = q->kf;
+    });
+}
+int ldsp_freqdem_demodulate(ldsp_freqdem_t q, const void* x, size_t n, void* y, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "freqdem_demodulate: NULL buffer");
+        if (q->device < 0) {
+            const int dev = current_device();
+            for (int i = 0; i < 2; i++) zero_now(q->prev[i].ensure(8, dev), 0, 8);
+            q->device = dev;
+        }
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const void* dx = q->stg.dev_in(e, x, n * 8);
+        float* dy = (float*)q->stg.dev_out(e, y, n * 4);
+        if (n > 0) {
+            k::freqdem(dx, q->prev[q->cur].p, q->prev[1 - q->cur].p, n, q->ref, dy, e.stream);
+            q->cur = 1 - q->cur;
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, n * 4);
+    });
+}
+
+// ---------------------------------------------------------------- Delay
+int ldsp_delay_create(unsigned int nd, ldsp_delay_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(nd <= (1u << 26), "delay: nd too large");
+        std::unique_ptr<ldsp_delay_s> o(new ldsp_delay_s());
+        o->nd = nd;
+        *q = o.release();
+    });
+}
+int ldsp_delay_destroy(ldsp_delay_t q)
+{
+    return guard([&] {
+        if (q && q->last) (void)hipStreamSynchronize(q->last);
+        delete q;
+    });
+}
+int ldsp_delay_set_delay(ldsp_delay_t q, unsigned int nd)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(nd <= (1u << 26), "delay: nd too large");
+        q->nd = nd;
+        if (q->device < 0) return;
+        DeviceGuard g(q->device);
+        if (q->last) LDSP_HIP(hipStreamSynchronize(q->last));
+        q->zero();
+    });
+}
+int ldsp_delay_get_delay(ldsp_delay_t q, unsigned int* nd)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(nd);
+        *nd = q->nd;
+    });
+}
+int ldsp_delay_execute(ldsp_delay_t q, const void* x, size_t n, int cplx, void* y, int mem, void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(n == 0 || (x && y), "delay_execute: NULL buffer");
+        if (q->device < 0) {
+            q->device = current_device();
+            DeviceGuard g(q->device);
+            q->zero();
+        }
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const size_t es = cplx ? 8 : 4;
+        const void* dx = q->stg.dev_in(e, x, n * es);
+        void* dy = q->stg.dev_out(e, y, n * es);
+        if (n > 0) {
+            const int D = (int)q->nd + 1;
+            int& c = cplx ? q->cc : q->cr;
+            ldsp::DevBuf* h = cplx ? q->hc : q->hr;
+            k::delay(cplx != 0, dx, h[c].p, h[1 - c].p, n, D, dy, e.stream);
+            c = 1 - c;
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, n * es);
+    });
+}
+
+// ---------------------------------------------------------------- bytes_to_iq
+int ldsp_bytes_to_iq(const void* in, size_t nbytes, void* y, int mem, void* stream)
+{
+    static std::mutex mu;
+    static std::vector<std::unique_ptr<Staging>> stgs;   // per device, host-memory calls only
+    return guard([&] {
+        const size_t n = nbytes / 4;
+        LDSP_REQUIRE(n == 0 || (in && y), "bytes_to_iq: NULL buffer");
+        const int dev = current_device();
+        const Exec e = make_exec(dev, mem, stream);
+        std::unique_lock<std::mutex> lk(mu, std::defer_lock);
+        if (e.host) lk.lock();   // the staging buffers are shared by host-memory calls
+        if ((int)stgs.size() <= dev) stgs.resize(dev + 1);
+        if (!stgs[dev]) stgs[dev].reset(new Staging());
+        Staging& stg = *stgs[dev];
+        const void* dx = stg.dev_in(e, in, n * 4);
+        void* dy = stg.dev_out(e, y, n * 8);
+        k::bytes_to_iq(dx, dy, n, e.stream);
+        stg.finish(e, y, n * 8);
     });
 }
 

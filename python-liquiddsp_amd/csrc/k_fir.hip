@@ -271,7 +271,14 @@ __device__ __forceinline__ void rs_mac(float2& r, float2 h, float2 v)
     r.y = r.y + (h.x * v.y + h.y * v.x);
 }
 
-template <bool CPLX>
+// real taps on complex samples (crcf): componentwise sequential accumulation
+__device__ __forceinline__ void rs_mac_cr(float2& r, float h, float2 v)
+{
+    r.x = r.x + h * v.x;
+    r.y = r.y + h * v.y;
+}
+
+template <bool CPLX, bool RT = false>
 __global__ void __launch_bounds__(64) k_resamp(const void* __restrict__ xv_, const void* __restrict__ hist_,
                                                void* __restrict__ hist_out_, long n, const float* __restrict__ sub,
                                                ResampPlan p, void* __restrict__ y_)
@@ -311,7 +318,12 @@ __global__ void __launch_bounds__(64) k_resamp(const void* __restrict__ xv_, con
     const uint64_t ph = p.P0 + (uint64_t)k * p.step - ((uint64_t)j << 24);
     const int b = (int)(ph >> p.bits_index);
     const int off = (int)(j - halo - jlo);
-    if constexpr (CPLX) {
+    if constexpr (CPLX && RT) {
+        const float* hb = sub + (size_t)b * p.sub_len;
+        float2 r = make_float2(0.0f, 0.0f);
+        for (int i = 0; i < p.sub_len; i++) rs_mac_cr(r, hb[i], lds[off + i]);
+        y[k] = r;
+    } else if constexpr (CPLX) {
         const float2* hb = reinterpret_cast<const float2*>(sub) + (size_t)b * p.sub_len;
         float2 r = make_float2(0.0f, 0.0f);
         for (int i = 0; i < p.sub_len; i++) rs_mac(r, hb[i], lds[off + i]);
@@ -329,19 +341,20 @@ __global__ void __launch_bounds__(64) k_resamp(const void* __restrict__ xv_, con
 // outputs' windows are ~1/rate samples apart, so a wave's loads touch ~64 lines
 // per instruction but every line is fetched from HBM once and re-read from L1;
 // no LDS staging or workgroup barrier sits between the loads and the math.
-template <bool CPLX>
+template <bool CPLX, bool RT = false>
 __global__ void __launch_bounds__(256) k_resamp_direct(const void* __restrict__ xv_, const void* __restrict__ hist_,
                                                        void* __restrict__ hist_out_, long n,
                                                        const float* __restrict__ sub, ResampPlan p,
                                                        void* __restrict__ y_)
 {
     using T = typename std::conditional<CPLX, float2, float>::type;
+    using TT = typename std::conditional<CPLX && !RT, float2, float>::type;   // tap type
     const T* __restrict__ x = (const T*)xv_;
     const T* __restrict__ hist = (const T*)hist_;
     T* hist_out = (T*)hist_out_;
     T* y = (T*)y_;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    T* taps = reinterpret_cast<T*>(smem);                  // [npfb][sub_len]
+    TT* taps = reinterpret_cast<TT*>(smem);                // [npfb][sub_len]
     const int tid = threadIdx.x;
     const int halo = p.sub_len - 1;
     if (blockIdx.x == 0) {
@@ -350,7 +363,7 @@ __global__ void __launch_bounds__(256) k_resamp_direct(const void* __restrict__ 
             hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
         }
     }
-    const T* subT = (const T*)sub;
+    const TT* subT = (const TT*)sub;
     for (int i = tid; i < p.npfb * p.sub_len; i += 256) taps[i] = subT[i];
     __syncthreads();
     const long k = (long)blockIdx.x * 256 + tid;
@@ -358,20 +371,22 @@ __global__ void __launch_bounds__(256) k_resamp_direct(const void* __restrict__ 
     const long j = resamp_j(p.P0, k, p.step);
     const uint64_t ph = p.P0 + (uint64_t)k * p.step - ((uint64_t)j << 24);
     const int b = (int)(ph >> p.bits_index);
-    const T* hb = taps + (size_t)b * p.sub_len;
+    const TT* hb = taps + (size_t)b * p.sub_len;
     const long g0 = j - halo;
     T r{};
     if (g0 >= 0) {
         const T* xb = x + g0;
         for (int i = 0; i < p.sub_len; i++) {
-            if constexpr (CPLX) rs_mac(r, hb[i], xb[i]);
+            if constexpr (CPLX && RT) rs_mac_cr(r, hb[i], xb[i]);
+            else if constexpr (CPLX) rs_mac(r, hb[i], xb[i]);
             else r = r + hb[i] * xb[i];
         }
     } else {
         for (int i = 0; i < p.sub_len; i++) {
             const long gi = g0 + i;
             const T v = gi >= 0 ? x[gi] : hist[gi + halo];
-            if constexpr (CPLX) rs_mac(r, hb[i], v);
+            if constexpr (CPLX && RT) rs_mac_cr(r, hb[i], v);
+            else if constexpr (CPLX) rs_mac(r, hb[i], v);
             else r = r + hb[i] * v;
         }
     }
@@ -380,41 +395,49 @@ __global__ void __launch_bounds__(256) k_resamp_direct(const void* __restrict__ 
 
 } // namespace
 
-void resamp(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
+void resamp(bool cplx, bool real_taps, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
             const ResampPlan& p, void* y, hipStream_t s)
 {
     const size_t elem = cplx ? 8 : 4;
-    const size_t tap_lds = (size_t)p.npfb * p.sub_len * elem;
-    if (tap_lds <= 32 * 1024 && p.K > 0) {
+    const size_t tap_lds = (size_t)p.npfb * p.sub_len * ((cplx && !real_taps) ? 8 : 4);
+    if (tap_lds <= 64 * 1024 && p.K > 0) {
         const unsigned g = (unsigned)((p.K + 255) / 256);
         LDSP_PROF(s, "k_resamp");
-        if (cplx)
+        if (cplx && real_taps) {
+            LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp_direct<true, true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)tap_lds));
+            hipLaunchKernelGGL((k_resamp_direct<true, true>), dim3(g), dim3(256), tap_lds, s, x, hist, hist_out,
+                               (long)n, sub, p, y);
+        } else if (cplx) {
+            LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp_direct<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)tap_lds));
             hipLaunchKernelGGL(k_resamp_direct<true>, dim3(g), dim3(256), tap_lds, s, x, hist, hist_out, (long)n, sub,
                                p, y);
-        else
+        } else {
+            LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp_direct<false>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)tap_lds));
             hipLaunchKernelGGL(k_resamp_direct<false>, dim3(g), dim3(256), tap_lds, s, x, hist, hist_out, (long)n,
                                sub, p, y);
+        }
         LDSP_HIP(hipGetLastError());
         return;
     }
+    // very large branch tables: stage each group's input span in LDS instead
     const size_t lds = (size_t)p.span_max * elem;
     const unsigned grid = (unsigned)std::max<size_t>(1, (p.K + p.KB - 1) / p.KB);
-    if (cplx) {
-        if (lds > 64 * 1024)
-            LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds));
-        {
-            LDSP_PROF(s, "k_resamp");
-            hipLaunchKernelGGL(k_resamp<true>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
-        }
+    auto go = [&](const void* fn) {
+        if (lds > 64 * 1024) LDSP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    };
+    LDSP_PROF(s, "k_resamp");
+    if (cplx && real_taps) {
+        go((const void*)k_resamp<true, true>);
+        hipLaunchKernelGGL((k_resamp<true, true>), dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
+    } else if (cplx) {
+        go((const void*)k_resamp<true>);
+        hipLaunchKernelGGL(k_resamp<true>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
     } else {
-        if (lds > 64 * 1024)
-            LDSP_HIP(hipFuncSetAttribute((const void*)k_resamp<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds));
-        {
-            LDSP_PROF(s, "k_resamp");
-            hipLaunchKernelGGL(k_resamp<false>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
-        }
+        go((const void*)k_resamp<false>);
+        hipLaunchKernelGGL(k_resamp<false>, dim3(grid), dim3(64), lds, s, x, hist, hist_out, (long)n, sub, p, y);
     }
     LDSP_HIP(hipGetLastError());
 }

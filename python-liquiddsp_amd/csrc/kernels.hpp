@@ -44,8 +44,8 @@ struct ResampPlan {
     int KB;               // outputs per workgroup
     int span_max;         // LDS samples per workgroup
 };
-// sub: [npfb][sub_len] branch taps reversed (cplx: complex64 with imag, rrrf: float)
-void resamp(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
+// sub: [npfb][sub_len] branch taps reversed (cccf: complex64 with imag 0; rrrf, crcf: float)
+void resamp(bool cplx, bool real_taps, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
             const ResampPlan& p, void* y, hipStream_t s);
 
 // ------------------------------------------------------------------ NCO
@@ -147,6 +147,11 @@ void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_ou
 
 // ------------------------------------------------------------------ debug
 void math_eval(int fn, const float* a, const float* b, float* y, size_t n, hipStream_t s);
+
+// k_misc.hip: bytes_to_iq, delay line, frequency discriminator
+void bytes_to_iq(const void* x, void* y, size_t n, hipStream_t s);
+void delay(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, int D, void* y, hipStream_t s);
+void freqdem(const void* x, const void* prev, void* prev_out, size_t n, float ref, float* y, hipStream_t s);
 
 } // namespace k
 } // namespace ldsp

@@ -255,6 +255,11 @@ struct Resampler {
         if (nf < 1) throw py::value_error("resampler: nfilter must be >= 1");
         check(ldsp_resamp_create(r, (unsigned)d, fc, sbsp, (unsigned)nf, c ? 1 : 0, &q));
     }
+    // resamp_*_create_default(rate) (RResampler / CResampler, resampler.hpp:10-13,46-49); kind 0 rrrf, 2 crcf
+    Resampler(float r, int kind) : cplx(kind != 0), rate_(r), fc_(0.25f), as_(60.0f), m_(7), npfb_(256)
+    {
+        check(ldsp_resamp_create_default(r, kind, &q));
+    }
     Resampler(const Resampler&) = delete;
     ~Resampler() { if (q) ldsp_resamp_destroy(q); }
     void reset() { check(ldsp_resamp_reset(q)); }
@@ -617,12 +622,141 @@ struct AmpModem {
 };
 
 
+// ------------------------------------------------------------------ BroadcastAM (demod.hpp:93-153)
+struct BroadcastAM {
+    ldsp_bcastam_t q = nullptr;
+    explicit BroadcastAM(int m)
+    {
+        if (m < 1) throw py::value_error("BroadcastAM: slen must be >= 1");
+        check(ldsp_bcastam_create((unsigned)m, &q));
+    }
+    BroadcastAM(const BroadcastAM&) = delete;
+    ~BroadcastAM()
+    {
+        if (q) ldsp_bcastam_destroy(q);
+    }
+    void reset() { check(ldsp_bcastam_reset(q)); }
+    bool get_exact()
+    {
+        int m = 0;
+        check(ldsp_bcastam_get_mode(q, &m));
+        return m == LDSP_MODE_EXACT;
+    }
+    void set_exact(bool e) { check(ldsp_bcastam_set_mode(q, e ? LDSP_MODE_EXACT : LDSP_MODE_FAST)); }
+    py::object call(const py::handle& x)
+    {
+        return run_same(x, true, false, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            return ldsp_bcastam_demodulate(q, xi, n, yo, nullptr, mem, s);
+        });
+    }
+};
+
+// ------------------------------------------------------------------ FreqDem (demod.hpp:189-219)
+struct FreqDem {
+    ldsp_freqdem_t q = nullptr;
+    float kf;
+    explicit FreqDem(float k) : kf(k) { check(ldsp_freqdem_create(k, &q)); }
+    FreqDem(const FreqDem&) = delete;
+    ~FreqDem()
+    {
+        if (q) ldsp_freqdem_destroy(q);
+    }
+    void reset() { check(ldsp_freqdem_reset(q)); }
+    void print() { py::print(py::str("freqdem:\n    mod. factor :  {:8.4f}").format(kf)); }
+    py::object call(const py::handle& x)
+    {
+        return run_same(x, true, false, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            return ldsp_freqdem_demodulate(q, xi, n, yo, mem, s);
+        });
+    }
+};
+
+// ------------------------------------------------------------------ Delay (utility.hpp:5-57)
+struct Delay {
+    ldsp_delay_t q = nullptr;
+    explicit Delay(int nd)
+    {
+        if (nd < 0) throw py::value_error("Delay: nd must be >= 0");
+        check(ldsp_delay_create((unsigned)nd, &q));
+    }
+    Delay(const Delay&) = delete;
+    ~Delay()
+    {
+        if (q) ldsp_delay_destroy(q);
+    }
+    int get_delay()
+    {
+        unsigned nd = 0;
+        check(ldsp_delay_get_delay(q, &nd));
+        return (int)nd;
+    }
+    void set_delay(int nd)
+    {
+        if (nd < 0) throw py::value_error("Delay: nd must be >= 0");
+        check(ldsp_delay_set_delay(q, (unsigned)nd));
+    }
+    // dispatch on dtype like the reference: complex64 / float32, anything else -> None
+    py::object call(const py::handle& x)
+    {
+        py::object tp = py::getattr(x, "dtype");
+        int kind = -1;
+        if (is_device_tensor(x)) {
+            py::object& torch = torch_mod();
+            if (tp.equal(torch.attr("complex64"))) kind = 1;
+            else if (tp.equal(torch.attr("float32"))) kind = 0;
+        } else {
+            if (tp.equal(py::dtype("complex64"))) kind = 1;
+            else if (tp.equal(py::dtype("float32"))) kind = 0;
+        }
+        if (kind < 0) return py::none();
+        const bool c = kind == 1;
+        return run_same(x, c, c, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+            return ldsp_delay_execute(q, xi, n, c ? 1 : 0, yo, mem, s);
+        });
+    }
+};
+
+// bytes_to_iq (utility.hpp:61-69): bytes-like -> numpy complex64; a uint8/int16
+// device tensor -> complex64 device tensor
+py::object bytes_to_iq(const py::handle& b)
+{
+    if (is_device_tensor(b)) {
+        py::object& torch = torch_mod();
+        py::object t = py::reinterpret_borrow<py::object>(b).attr("reshape")(-1).attr("contiguous")();
+        const size_t nbytes = t.attr("numel")().cast<size_t>() * t.attr("element_size")().cast<size_t>();
+        py::object dev = t.attr("device");
+        void* s = reinterpret_cast<void*>(
+            torch.attr("cuda").attr("current_stream")(dev).attr("cuda_stream").cast<uintptr_t>());
+        py::object out = dev_empty(nbytes / 4, true, dev);
+        check(ldsp_bytes_to_iq(tptr(t), nbytes, tptr(out), LDSP_MEM_DEVICE, s));
+        return out;
+    }
+    py::buffer_info bi = py::reinterpret_borrow<py::buffer>(b).request();
+    const size_t nbytes = (size_t)bi.size * (size_t)bi.itemsize;
+    py::array_t<cf> out(nbytes / 4);
+    void* yp = out.mutable_data();
+    int rc;
+    {
+        py::gil_scoped_release rel;
+        rc = ldsp_bytes_to_iq(bi.ptr, nbytes, yp, LDSP_MEM_HOST, nullptr);
+    }
+    check(rc);
+    return std::move(out);
+}
+
 // distinct C++ types for the distinct Python classes
 struct RealResampler : Resampler {
     RealResampler(float r, int d, float fc, float as, int nf) : Resampler(r, d, fc, as, nf, false) {}
 };
 struct ComplexResampler : Resampler {
     ComplexResampler(float r, int d, float fc, float as, int nf) : Resampler(r, d, fc, as, nf, true) {}
+};
+// RResampler / CResampler (resampler.hpp:4-70): default designs, rate only
+struct RResampler : Resampler {
+    explicit RResampler(float r) : Resampler(r, 0) {}
+};
+struct CResampler : Resampler {
+    explicit CResampler(float r) : Resampler(r, 2) {}
 };
 struct CIIRFilter : TFIIR {
     CIIRFilter(const py::handle& b, const py::handle& a) : TFIIR(b, a, true) {}
@@ -798,6 +932,35 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("__call__", [](NCO& n, const py::handle& x) { return n.mix(x, false); })
         .def("mix_up", [](NCO& n, const py::handle& x) { return n.mix(x, false); })
         .def("mix_down", [](NCO& n, const py::handle& x) { return n.mix(x, true); });
+
+    // ---- bytes_to_iq, Delay (wrapper.cpp:13, 25-28)
+    m.def("bytes_to_iq", &bytes_to_iq, py::arg("byts"));
+    py::class_<Delay>(m, "Delay")
+        .def(py::init<int>(), py::arg("nd") = 1)
+        .def_property("delay", &Delay::get_delay, &Delay::set_delay)
+        .def("__call__", &Delay::call);
+
+    // ---- FreqDem (wrapper.cpp:183-187), BroadcastAM (wrapper.cpp:259-262)
+    py::class_<FreqDem>(m, "FreqDem")
+        .def(py::init<float>())
+        .def("reset", &FreqDem::reset)
+        .def("print", &FreqDem::print)
+        .def("__call__", &FreqDem::call);
+    py::class_<BroadcastAM>(m, "BroadcastAM")
+        .def(py::init<int>(), py::arg("slen") = 25)
+        .def("reset", &BroadcastAM::reset)
+        .def_property("exact", &BroadcastAM::get_exact, &BroadcastAM::set_exact)
+        .def("__call__", &BroadcastAM::call);
+
+    // ---- RResampler / CResampler (wrapper.cpp:15-23)
+    py::class_<RResampler>(m, "RResampler")
+        .def(py::init<float>(), py::arg("rate"))
+        .def("reset", &RResampler::reset)
+        .def("__call__", &RResampler::call);
+    py::class_<CResampler>(m, "CResampler")
+        .def(py::init<float>(), py::arg("rate"))
+        .def("reset", &CResampler::reset)
+        .def("__call__", &CResampler::call);
 
     // ---- RealResampler / ComplexResampler (wrapper.cpp:214-226)
     py::class_<RealResampler>(m, "RealResampler", kResampDoc)

@@ -378,6 +378,88 @@ def test_ampmodem_bitwise(ld, ora, rng, carrier):
     assert g.pll_state() == o.pll_state
 
 
+
+# ------------------------------------------------------------------ helpers either side of the path
+def test_bytes_to_iq_bitwise(ld, ora, rng):
+    import torch
+    raw = rng.integers(-32768, 32767, size=2 * 300_001, dtype=np.int16)
+    for b in (raw.tobytes(), raw.tobytes() + b"\x01\x02\x03", b"", b"\x05\x06"):
+        assert_bitwise(ld.bytes_to_iq(b), ora.bytes_to_iq(b))
+    yd = ld.bytes_to_iq(torch.from_numpy(raw).cuda())
+    assert yd.is_cuda and yd.dtype == torch.complex64
+    assert_bitwise(yd.cpu().numpy(), ora.bytes_to_iq(raw.tobytes()))
+
+
+@pytest.mark.parametrize("nd", [0, 1, 7, 1000])
+def test_delay_bitwise_streaming(ld, ora, rng, nd):
+    g, o = ld.Delay(nd), ora.Delay(nd)
+    assert g.delay == nd
+    x = cgauss(rng, 20_000)
+    r = np.float32(rng.standard_normal(9_000))
+    cuts = [0, 1, 5, 600, 601, 4000, 20_000]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        assert_bitwise(g(x[a:b]), o(x[a:b]))
+        assert_bitwise(g(r[a % 9000:a % 9000 + 300]), o(r[a % 9000:a % 9000 + 300]))
+    assert g(np.zeros(3, np.int32)) is None
+    g.delay = 3
+    o.delay = 3
+    assert_bitwise(g(x[:50]), o(x[:50]))
+
+
+def test_delay_device_tensor(ld, ora, rng):
+    import torch
+    g, o = ld.Delay(5), ora.Delay(5)
+    x = cgauss(rng, 1000)
+    y = g(torch.from_numpy(x).cuda())
+    assert y.is_cuda and y.dtype == torch.complex64
+    assert_bitwise(y.cpu().numpy(), o(x))
+
+
+@pytest.mark.parametrize("kf", [0.05, 0.3])
+def test_freqdem_bitwise(ld, ora, rng, kf):
+    x = cgauss(rng, 300_000)
+    x[1000:1010] = 0                           # cargf(0) cases
+    g, o = ld.FreqDem(kf), ora.FreqDem(kf)
+    y = np.concatenate([g(x[:1]), g(x[1:77_777]), g(x[77_777:])])
+    assert_bitwise(y, o(x))
+    g.reset()
+    o.reset()
+    assert_bitwise(g(x[:5000]), o(x[:5000]))
+
+
+def test_broadcast_am_exact_bitwise(ld, ora, rng):
+    x = _am(rng, 200_000, 48000.0, 3.0, amp=1.0)
+    g = ld.BroadcastAM(slen=25)
+    g.exact = True
+    o = ora.BroadcastAM(25)
+    y = np.concatenate([g(x[:4321]), g(x[4321:])])
+    assert_bitwise(y, o(x))
+    g.reset()
+    o.reset()
+    assert_bitwise(g(x[:9000]), o(x[:9000]))
+
+
+def test_broadcast_am_fast_close(ld, ora, rng):
+    # fast mode: PLL stage bit-exact, DC blocker = float64 scan; compared with
+    # the same stage evaluated in float64 on the CPU
+    x = _am(rng, 1 << 20, 48000.0, 3.0, amp=1.0)
+    g = ld.BroadcastAM()
+    assert not g.exact
+    y = g(x)
+    ref = ora.BroadcastAM(25, iir_f64=True)(x)
+    assert maxrel(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize("rate", [0.024, 0.5, 1.3])
+def test_default_resamplers_bitwise(ld, ora, rng, rate):
+    # RResampler = resamp_rrrf_create_default, CResampler = resamp_crcf_create_default
+    x = cgauss(rng, 50_000)
+    r = np.float32(rng.standard_normal(50_000))
+    gc, oc = ld.CResampler(rate), ora.Resampler(rate, cplx=True, real_taps=True, default=True)
+    gr, orr = ld.RResampler(rate), ora.Resampler(rate, cplx=False, default=True)
+    assert_bitwise(np.concatenate([gc(x[:999]), gc(x[999:])]), oc(x))
+    assert_bitwise(np.concatenate([gr(r[:12345]), gr(r[12345:])]), orr(r))
+
 # ------------------------------------------------------------------ chain
 def _chain(ld, exact):
     bandpass = ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2000000)
