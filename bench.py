@@ -313,7 +313,29 @@ def components(L, device, reps=5):
                                "fir_GBs": round(16 * n / t[fk] / 1e6, 1),
                                "Msamples_s": round(n / (t["k_nco_mix"] + t[fk]) / 1e3, 1)}
     del xs
+    out["host_buffers"] = host_path(L, device)
     return out
+
+
+def host_path(L, device, n=16 << 20, reps=3):
+    """PCIe-inclusive rates of the AM chain when the caller hands over host
+    buffers (never `value`): (a) one H2D copy of the IQ block, the chain on the
+    device, one D2H copy of the PCM; (b) the README callback on numpy arrays,
+    where every stage stages its input to HBM and its output back."""
+    xh = synth_channel(n, 0, device).cpu().numpy()
+    res = {"iq_samples": n}
+    for name, fn in (("h2d_chain_d2h", lambda r: r(torch.from_numpy(xh).to(device)).cpu()),
+                     ("numpy_every_stage", lambda r: r(xh))):
+        radio = AMRadio(L)
+        fn(radio)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn(radio)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / reps
+        res[name] = {"ms": round(el * 1e3, 2), "Msamples_s": round(n / el / 1e6, 1)}
+    return res
 
 
 if __name__ == "__main__":

@@ -247,6 +247,24 @@ int ldsp_freqdem_get_kf(ldsp_freqdem_t q, float *kf);
 int ldsp_freqdem_demodulate(ldsp_freqdem_t q, const void *x, size_t n, void *y, int mem, void *stream);
 
 /* ------------------------------------------------------------------------
+ * FM stereo receiver.  Replaces FMStereo (src/demod.hpp:4-85, wrapper.cpp:264-267):
+ * freqdem(4) -> composite mixer loop (NCO, PLL bandwidth 0.1, one-pole phase
+ * error) -> 75 us de-emphasis per channel -> resamp_rrrf_create_default
+ * (pcm_rate / iq_rate) per channel; output interleaved (L, R) float32.
+ * Bit-exact; the mixer loop is inherently sequential (one lane).  reset()
+ * resets only the resamplers, like the reference.  pcm_rate > iq_rate is
+ * LDSP_EUNSUP.  num_outputs counts floats (2 per output pair).
+ * ---------------------------------------------------------------------- */
+typedef struct ldsp_fmstereo_s *ldsp_fmstereo_t;
+int ldsp_fmstereo_create(float iq_rate, float pcm_rate, ldsp_fmstereo_t *q);
+int ldsp_fmstereo_destroy(ldsp_fmstereo_t q);
+int ldsp_fmstereo_reset(ldsp_fmstereo_t q);
+int ldsp_fmstereo_num_outputs(ldsp_fmstereo_t q, size_t n, size_t *nout);
+int ldsp_fmstereo_get_state(ldsp_fmstereo_t q, uint32_t *theta, uint32_t *dtheta, float *pe);
+int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void *x, size_t n, void *y, size_t cap, size_t *nout,
+                          int mem, void *stream);
+
+/* ------------------------------------------------------------------------
  * Sample delay line.  Replaces Delay (src/utility.hpp:5-57, wrapper.cpp:25-28):
  * separate real (wdelayf) and complex (wdelaycf) lines of nd, read-then-push,
  * i.e. y[n] = x[n - nd - 1].  set_delay re-creates (zeroes) both lines.

@@ -1551,3 +1551,99 @@ void ora_bcastam_demodulate_block(ora_bcastam q, const float *x, size_t n, float
     if (iir_f64) ora_iirfilt_execute_block_f64(q->dcblock, pre, n, y);
     else ora_iirfilt_execute_block(q->dcblock, pre, n, y);
 }
+
+/* ===================================================================== */
+/* FMStereo: reference src/demod.hpp:4-85 (python-liquiddsp's own loop)   */
+/*   s = freqdem(x) (kf 4);  sc = s e^{-j theta};                         */
+/*   pe = 0.999 pe + 0.001 carg(sc)   (double arithmetic, stored float);  */
+/*   sc = sc e^{-j theta}; nco_pll_step(pe) (bandwidth 0.1); theta += d;  */
+/*   L/R = de-emphasis(s +- re(sc)) -> resamp_rrrf_create_default(pcm/iq) */
+/* An (L, R) pair is appended only when each resampler produced exactly   */
+/* one output (demod_one returns nl + nr == 2, demod.hpp:45-47).          */
+/* reset() resets only the two resamplers (demod.hpp:34-37); phase_error */
+/* is uninitialised in the reference and starts at 0 here.               */
+/* ===================================================================== */
+struct ora_fmstereo_s {
+    ora_nco mixer;
+    ora_freqdem dem;
+    ora_iirfilt emph_l, emph_r;
+    ora_resamp aud_l, aud_r;
+    float pe;
+};
+ora_fmstereo ora_fmstereo_create(float iq_rate, float pcm_rate)
+{
+    ora_fmstereo q = (ora_fmstereo)calloc(1, sizeof(*q));
+    float b[1], a[2];
+    a[0] = 1.0;
+    a[1] = -exp(-1.0 / (75.0E-6 * iq_rate));
+    b[0] = 1.0 + a[1];
+    q->mixer = ora_nco_create(0);
+    q->dem = ora_freqdem_create(4.0f);
+    q->emph_l = ora_iirfilt_create_tf(b, 1, a, 2, 0);
+    q->emph_r = ora_iirfilt_create_tf(b, 1, a, 2, 0);
+    q->aud_l = ora_resamp_create_default(pcm_rate / iq_rate, 0);
+    q->aud_r = ora_resamp_create_default(pcm_rate / iq_rate, 0);
+    q->pe = 0.0f;
+    return q;
+}
+void ora_fmstereo_destroy(ora_fmstereo q)
+{
+    if (!q) return;
+    ora_nco_destroy(q->mixer);
+    ora_freqdem_destroy(q->dem);
+    ora_iirfilt_destroy(q->emph_l);
+    ora_iirfilt_destroy(q->emph_r);
+    ora_resamp_destroy(q->aud_l);
+    ora_resamp_destroy(q->aud_r);
+    free(q);
+}
+void ora_fmstereo_reset(ora_fmstereo q)
+{
+    ora_resamp_reset(q->aud_l);
+    ora_resamp_reset(q->aud_r);
+}
+void ora_fmstereo_get_state(ora_fmstereo q, uint32_t *theta, uint32_t *dtheta, float *pe)
+{
+    *theta = q->mixer->theta;
+    *dtheta = q->mixer->d_theta;
+    *pe = q->pe;
+}
+void ora_fmstereo_set_state(ora_fmstereo q, uint32_t theta, uint32_t dtheta, float pe)
+{
+    q->mixer->theta = theta;
+    q->mixer->d_theta = dtheta;
+    q->pe = pe;
+}
+size_t ora_fmstereo_execute(ora_fmstereo q, const float *x, size_t n, float *y, float *dbg)
+{
+    size_t i, nw = 0;
+    for (i = 0; i < n; i++) {
+        float s, c, sn, r1, i1, r2, i2, l, r, lo[8], ro[8];
+        ora_freqdem_demodulate_block(q->dem, x + 2 * i, 1, &s);
+        nco_sincos(q->mixer, &sn, &c);
+        cmul_down(s, 0.0f, c, sn, &r1, &i1);                  /* mix_down of (s + 0j) */
+        q->pe = 0.999 * q->pe + 0.001 * om_atan2f(i1, r1);    /* double, stored float */
+        cmul_down(r1, i1, c, sn, &r2, &i2);                   /* same phase: down again */
+        ora_nco_pll_step(q->mixer, q->pe);
+        q->mixer->theta += q->mixer->d_theta;                 /* nco_crcf_step */
+        if (dbg) {
+            dbg[4 * i] = s;
+            dbg[4 * i + 1] = r2;
+            dbg[4 * i + 2] = q->pe;
+            uint32_t th = q->mixer->theta;
+            memcpy(&dbg[4 * i + 3], &th, 4);
+        }
+        l = s + r2;
+        r = s - r2;
+        ora_iirfilt_execute_block(q->emph_l, &l, 1, &l);
+        ora_iirfilt_execute_block(q->emph_r, &r, 1, &r);
+        size_t nl = ora_resamp_execute_block(q->aud_l, &l, 1, lo);
+        size_t nr = ora_resamp_execute_block(q->aud_r, &r, 1, ro);
+        if (nl + nr == 2) {
+            y[nw] = lo[0];
+            y[nw + 1] = ro[0];
+            nw += 2;
+        }
+    }
+    return nw;
+}

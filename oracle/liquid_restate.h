@@ -155,6 +155,18 @@ void ora_bcastam_destroy(ora_bcastam q);
 void ora_bcastam_reset(ora_bcastam q);
 void ora_bcastam_demodulate_block(ora_bcastam q, const float *x, size_t n, float *pre, float *y, int iir_f64);
 
+/* ---- FMStereo (src/demod.hpp:4-85) ------------------------------------ */
+typedef struct ora_fmstereo_s *ora_fmstereo;
+ora_fmstereo ora_fmstereo_create(float iq_rate, float pcm_rate);
+void ora_fmstereo_destroy(ora_fmstereo q);
+void ora_fmstereo_reset(ora_fmstereo q);
+/* y: interleaved (L, R) pairs, capacity 2 n; returns the number of floats written.
+ * dbg (optional, 4 n floats): per sample s, re(sc) after the second mix, the
+ * phase error, theta bits (internal checks) */
+size_t ora_fmstereo_execute(ora_fmstereo q, const float *x, size_t n, float *y, float *dbg);
+void ora_fmstereo_get_state(ora_fmstereo q, uint32_t *theta, uint32_t *dtheta, float *pe);
+void ora_fmstereo_set_state(ora_fmstereo q, uint32_t theta, uint32_t dtheta, float pe);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,12 @@ def _load():
         "ora_bcastam_destroy": (None, [vp]),
         "ora_bcastam_reset": (None, [vp]),
         "ora_bcastam_demodulate_block": (None, [vp, f32p, sz, f32p, f32p, i]),
+        "ora_fmstereo_create": (vp, [f, f]),
+        "ora_fmstereo_destroy": (None, [vp]),
+        "ora_fmstereo_reset": (None, [vp]),
+        "ora_fmstereo_execute": (sz, [vp, f32p, sz, f32p, vp]),
+        "ora_fmstereo_get_state": (None, [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(f)]),
+        "ora_fmstereo_set_state": (None, [vp, u32, u32, f]),
         "ora_resamp_destroy": (None, [vp]),
         "ora_resamp_reset": (None, [vp]),
         "ora_resamp_set_rate": (i, [vp, f]),
@@ -575,6 +581,40 @@ class BroadcastAM(_Handle):
         y = np.empty(len(x), np.float32)
         lib().ora_bcastam_demodulate_block(self._h, xf, len(x), pre, y, self.iir_f64)
         return (pre, y) if return_pre else y
+
+
+class FMStereo(_Handle):
+    """FMStereo (src/demod.hpp:4-85): freqdem(4) -> composite PLL mixer ->
+    75 us de-emphasis -> resamp_rrrf default, (L, R) interleaved float32.
+    __call__(x, debug=True) also returns per-sample [s, re(sc), pe, theta bits]."""
+    _destroy = "ora_fmstereo_destroy"
+
+    def __init__(self, iq_rate=600000.0, pcm_rate=48000.0):
+        self._h = lib().ora_fmstereo_create(iq_rate, pcm_rate)
+
+    def reset(self):
+        lib().ora_fmstereo_reset(self._h)
+
+    @property
+    def state(self):
+        t, d, p = C.c_uint32(), C.c_uint32(), C.c_float()
+        lib().ora_fmstereo_get_state(self._h, C.byref(t), C.byref(d), C.byref(p))
+        return t.value, d.value, p.value
+
+    @state.setter
+    def state(self, v):
+        lib().ora_fmstereo_set_state(self._h, int(v[0]) & 0xffffffff, int(v[1]) & 0xffffffff, float(v[2]))
+
+    def __call__(self, x, debug=False):
+        xf = _c64_as_f32(x)
+        y = np.empty(2 * len(x) + 2, np.float32)
+        dbg = np.empty(4 * len(x) + 1, np.float32) if debug else None
+        nw = lib().ora_fmstereo_execute(self._h, xf, len(x), y, dbg.ctypes.data if debug else None)
+        y = y[:nw].copy()
+        if debug:
+            d = dbg[:4 * len(x)].reshape(-1, 4)
+            return y, d
+        return y
 
 
 class Delay:

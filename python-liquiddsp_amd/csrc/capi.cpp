@@ -610,6 +610,21 @@ struct ldsp_freqdem_s {
     ldsp::Staging stg;
 };
 
+// FMStereo (demod.hpp:4-85): freqdem(4) + mixer loop + two TF de-emphasis
+// filters (exact) + two resamp_rrrf_create_default resamplers.
+struct ldsp_fmstereo_s {
+    float iq_rate = 0, pcm_rate = 0;
+    ldsp_freqdem_t dem = nullptr;
+    ldsp_iirfilt_t emph[2] = {nullptr, nullptr};
+    ldsp_resamp_t aud[2] = {nullptr, nullptr};
+    std::vector<float> table;
+    ldsp::k::FmState st{};
+    int device = -1;
+    ldsp::DevBuf dst, dtab, sbuf, lr[2], le[2], out[2];
+    hipStream_t last = nullptr;
+    ldsp::Staging stg;
+};
+
 struct ldsp_delay_s {
     unsigned int nd = 1;
     int device = -1, cr = 0, cc = 0;
@@ -1274,12 +1289,12 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
         void* dy = q->stg.dev_out(e, y, bytes);
         if (n > 0) {
             const k::IirDesc d = q->desc();
-            if (q->spec_W > 0 && q->spec_W <= 4096) {
+            if (q->spec_W > 0 && q->spec_W <= 16384) {
                 // fast-decaying filter: speculative exact chunks (same bits as sequential)
                 q->state_to(false, e.stream);
                 k::SpecPlan p;
                 p.W = q->spec_W;
-                p.C = 128;                       // chunks are cheap: W + C steps per lane
+                p.C = std::max(128, q->spec_W / 32);   // W + C steps per lane, <= 1/32 redundancy growth
                 p.nchunks = (long)((n + p.C - 1) / p.C);
                 const size_t need = k::spec_scratch_bytes(p.nchunks, q->ncomp(), q->fsz());
                 p.scratch = q->sc1.ensure(need, q->device);
@@ -1796,6 +1811,138 @@ int ldsp_delay_execute(ldsp_delay_t q, const void* x, size_t n, int cplx, void* 
         }
         q->last = e.stream;
         q->stg.finish(e, y, n * es);
+    });
+}
+
+// ---------------------------------------------------------------- FMStereo
+int ldsp_fmstereo_create(float iq_rate, float pcm_rate, ldsp_fmstereo_t* q)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(iq_rate > 0.0f && pcm_rate > 0.0f, "fmstereo: rates must be > 0");
+        const float rate = pcm_rate / iq_rate;
+        if (rate > 1.0f)
+            throw Error(LDSP_EUNSUP, "fmstereo: pcm_rate > iq_rate (the reference drops the samples of inputs that "
+                                     "produce two outputs, demod.hpp:45-47; not reproduced)");
+        std::unique_ptr<ldsp_fmstereo_s> o(new ldsp_fmstereo_s());
+        o->iq_rate = iq_rate;
+        o->pcm_rate = pcm_rate;
+        // demod.hpp:19-31: 75 us de-emphasis (double arithmetic stored as float)
+        float a[2], b[1];
+        a[0] = 1.0;
+        a[1] = -exp(-1.0 / (75.0E-6 * iq_rate));
+        b[0] = 1.0 + a[1];
+        auto ok = [](int rc) {
+            if (rc != LDSP_OK) throw Error(rc, g_last_error);
+        };
+        ok(ldsp_freqdem_create(4.0f, &o->dem));
+        for (int c = 0; c < 2; c++) {
+            ok(ldsp_iirfilt_create_tf(b, 1, a, 2, 0, &o->emph[c]));
+            ok(ldsp_iirfilt_set_mode(o->emph[c], LDSP_MODE_EXACT));
+            ok(ldsp_resamp_create_default(rate, 0, &o->aud[c]));
+        }
+        o->table = nco_table();
+        o->st.theta = 0;
+        o->st.dtheta = 0;
+        o->st.pe = 0.0f;           // uninitialised member in the reference (demod.hpp:13)
+        o->st.alpha = 0.1f;        // nco_crcf_create: PLL bandwidth 0.1
+        o->st.beta = sqrtf(0.1f);
+        *q = o.release();
+    });
+}
+int ldsp_fmstereo_destroy(ldsp_fmstereo_t q)
+{
+    return guard([&] {
+        if (!q) return;
+        if (q->last) (void)hipStreamSynchronize(q->last);
+        ldsp_freqdem_destroy(q->dem);
+        for (int c = 0; c < 2; c++) {
+            ldsp_iirfilt_destroy(q->emph[c]);
+            ldsp_resamp_destroy(q->aud[c]);
+        }
+        delete q;
+    });
+}
+int ldsp_fmstereo_reset(ldsp_fmstereo_t q)
+{
+    return guard([&] {
+        NONNULL(q);
+        for (int c = 0; c < 2; c++) {   // demod.hpp:34-37: only the resamplers
+            const int rc = ldsp_resamp_reset(q->aud[c]);
+            if (rc != LDSP_OK) throw Error(rc, g_last_error);
+        }
+    });
+}
+int ldsp_fmstereo_num_outputs(ldsp_fmstereo_t q, size_t n, size_t* nout)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(nout);
+        size_t k = 0;
+        const int rc = ldsp_resamp_num_outputs(q->aud[0], n, &k);
+        if (rc != LDSP_OK) throw Error(rc, g_last_error);
+        *nout = 2 * k;
+    });
+}
+int ldsp_fmstereo_get_state(ldsp_fmstereo_t q, uint32_t* theta, uint32_t* dtheta, float* pe)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (q->device >= 0) {
+            DeviceGuard g(q->device);
+            if (q->last) LDSP_HIP(hipStreamSynchronize(q->last));
+            LDSP_HIP(hipMemcpy(&q->st, q->dst.p, sizeof(q->st), hipMemcpyDeviceToHost));
+        }
+        if (theta) *theta = q->st.theta;
+        if (dtheta) *dtheta = q->st.dtheta;
+        if (pe) *pe = q->st.pe;
+    });
+}
+int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, size_t cap, size_t* nout, int mem,
+                          void* stream)
+{
+    return guard([&] {
+        NONNULL(q);
+        size_t k = 0;
+        int rc = ldsp_resamp_num_outputs(q->aud[0], n, &k);
+        if (rc != LDSP_OK) throw Error(rc, g_last_error);
+        if (nout) *nout = 2 * k;
+        if (2 * k > cap) throw Error(LDSP_ERANGE, "fmstereo_execute: output capacity too small");
+        LDSP_REQUIRE(n == 0 || x, "fmstereo_execute: NULL input");
+        LDSP_REQUIRE(k == 0 || y, "fmstereo_execute: NULL output");
+        if (q->device < 0) {
+            const int dev = current_device();
+            q->dst.ensure(sizeof(k::FmState), dev);
+            LDSP_HIP(hipMemcpy(q->dst.p, &q->st, sizeof(q->st), hipMemcpyHostToDevice));
+            upload(q->dtab, q->table, dev);
+            q->device = dev;
+        }
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream);
+        const void* dx = q->stg.dev_in(e, x, n * 8);
+        float* dy = (float*)q->stg.dev_out(e, y, 2 * k * 4);
+        if (n > 0) {
+            auto ok = [](int r) {
+                if (r != LDSP_OK) throw Error(r, g_last_error);
+            };
+            float* sd = (float*)q->sbuf.ensure(n * 4, q->device);
+            ok(ldsp_freqdem_demodulate(q->dem, dx, n, sd, LDSP_MEM_DEVICE, e.stream));
+            float* l = (float*)q->lr[0].ensure(n * 4, q->device);
+            float* r = (float*)q->lr[1].ensure(n * 4, q->device);
+            k::fm_pll(sd, n, q->dst.as<k::FmState>(), q->dtab.as<float>(), l, r, e.stream);
+            float* outs[2];
+            for (int c = 0; c < 2; c++) {
+                float* de = (float*)q->le[c].ensure(n * 4, q->device);
+                ok(ldsp_iirfilt_execute(q->emph[c], c ? r : l, n, de, LDSP_MEM_DEVICE, e.stream));
+                outs[c] = (float*)q->out[c].ensure(std::max<size_t>(k, 1) * 4, q->device);
+                size_t kc = 0;
+                ok(ldsp_resamp_execute(q->aud[c], de, n, outs[c], k, &kc, LDSP_MEM_DEVICE, e.stream));
+                LDSP_REQUIRE(kc == k, "fmstereo: resampler output counts diverged");
+            }
+            k::interleave2(outs[0], outs[1], k, dy, e.stream);
+        }
+        q->last = e.stream;
+        q->stg.finish(e, y, 2 * k * 4);
     });
 }
 

@@ -152,6 +152,12 @@ void math_eval(int fn, const float* a, const float* b, float* y, size_t n, hipSt
 void bytes_to_iq(const void* x, void* y, size_t n, hipStream_t s);
 void delay(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, int D, void* y, hipStream_t s);
 void freqdem(const void* x, const void* prev, void* prev_out, size_t n, float ref, float* y, hipStream_t s);
+struct FmState {          // FMStereo mixer loop state (device-resident)
+    uint32_t theta, dtheta;
+    float pe, alpha, beta;
+};
+void fm_pll(const float* s, size_t n, FmState* st, const float* table, float* l, float* r, hipStream_t strm);
+void interleave2(const float* a, const float* b, size_t n, float* y, hipStream_t strm);
 
 } // namespace k
 } // namespace ldsp

@@ -128,18 +128,15 @@ __host__ __device__ inline float lm_atanf_pos(float t)
     const bool lt0687 = ix < 0x3f300000u;
     const bool lt24375 = ix < 0x401c0000u;
     // id 0: (2t-1)/(2+t)  id 1: (t-1)/(t+1)  id 2: (t-1.5)/(1+1.5t)  id 3: -1/t
-    float num, den, hi, lo;
-    if (lt1875) {
-        num = lt0687 ? 2.0f * t - 1.0f : t - 1.0f;
-        den = lt0687 ? 2.0f + t : t + 1.0f;
-        hi = lt0687 ? 4.6364760399e-01f : 7.8539812565e-01f;
-        lo = lt0687 ? 5.0121582440e-09f : 3.7748947079e-08f;
-    } else {
-        num = lt24375 ? t - 1.5f : -1.0f;
-        den = lt24375 ? 1.0f + 1.5f * t : t;
-        hi = lt24375 ? 9.8279368877e-01f : 1.5707962513e+00f;
-        lo = lt24375 ? 3.4473217170e-08f : 7.5497894159e-08f;
-    }
+    // (selects, not branches: vectorised callers stay in one basic block)
+    const float n0 = 2.0f * t - 1.0f, n1 = t - 1.0f, n2 = t - 1.5f;
+    const float d0 = 2.0f + t, d1 = t + 1.0f, d2 = 1.0f + 1.5f * t;
+    float num = lt1875 ? (lt0687 ? n0 : n1) : (lt24375 ? n2 : -1.0f);
+    float den = lt1875 ? (lt0687 ? d0 : d1) : (lt24375 ? d2 : t);
+    const float hi = lt1875 ? (lt0687 ? 4.6364760399e-01f : 7.8539812565e-01f)
+                            : (lt24375 ? 9.8279368877e-01f : 1.5707962513e+00f);
+    const float lo = lt1875 ? (lt0687 ? 5.0121582440e-09f : 3.7748947079e-08f)
+                            : (lt24375 ? 3.4473217170e-08f : 7.5497894159e-08f);
     num = idm ? t : num;
     den = idm ? 1.0f : den;
     const float xr = num / den;                         // t / 1.0 == t exactly
@@ -167,19 +164,19 @@ __host__ __device__ inline float lm_atan2f(float y, float x)
     z = (hx < 0 && k < -26) ? 0.0f : z;
     z = (k > 26) ? pi_o_2 + 0.5f * pi_lo : z;
     const float zm = z - pi_lo;
-    float r = (m & 2) ? ((m & 1) ? zm - pi : pi - zm) : ((m & 1) ? -z : z);
-    if (iy == 0 || ix == 0 || ix >= 0x7f800000 || iy >= 0x7f800000) {   // rare special operands
-        if (ix > 0x7f800000 || iy > 0x7f800000) r = x + y;
-        else if (iy == 0) r = m <= 1 ? y : (m == 2 ? pi : -pi);
-        else if (ix == 0) r = (hy < 0) ? -pi_o_2 : pi_o_2;
-        else if (ix == 0x7f800000) {
-            if (iy == 0x7f800000)
-                r = m == 0 ? pi_o_4 : m == 1 ? -pi_o_4 : m == 2 ? 3.0f * pi_o_4 : -3.0f * pi_o_4;
-            else
-                r = m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi : -pi;
-        } else r = (hy < 0) ? -pi_o_2 : pi_o_2;         // y infinite
-    }
-    return r;
+    const float q2 = zm - pi, q1 = pi - zm;
+    float r = (m & 2) ? ((m & 1) ? q2 : q1) : ((m & 1) ? -z : z);
+    // special operands, as selects (no divergent branches inside vectorised callers)
+    const bool spec = iy == 0 || ix == 0 || ix >= 0x7f800000 || iy >= 0x7f800000;
+    const float r_pm2 = (hy < 0) ? -pi_o_2 : pi_o_2;
+    const float r_y0 = m <= 1 ? y : (m == 2 ? pi : -pi);
+    const float r_ii = m == 0 ? pi_o_4 : m == 1 ? -pi_o_4 : m == 2 ? 3.0f * pi_o_4 : -3.0f * pi_o_4;
+    const float r_ix = m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi : -pi;
+    float rs = ix == 0x7f800000 ? (iy == 0x7f800000 ? r_ii : r_ix) : r_pm2;
+    rs = ix == 0 ? r_pm2 : rs;
+    rs = iy == 0 ? r_y0 : rs;
+    rs = (ix > 0x7f800000 || iy > 0x7f800000) ? x + y : rs;
+    return spec ? rs : r;
 }
 
 // tanh: odd minimax polynomial below 0.625, 1 - 2/(e^{2|x|}+1) above

@@ -671,6 +671,54 @@ struct FreqDem {
     }
 };
 
+// ------------------------------------------------------------------ FMStereo (demod.hpp:4-85)
+struct FMStereo {
+    ldsp_fmstereo_t q = nullptr;
+    FMStereo(float iq_rate, float pcm_rate) { check(ldsp_fmstereo_create(iq_rate, pcm_rate, &q)); }
+    FMStereo(const FMStereo&) = delete;
+    ~FMStereo()
+    {
+        if (q) ldsp_fmstereo_destroy(q);
+    }
+    void reset() { check(ldsp_fmstereo_reset(q)); }
+    py::tuple state()
+    {
+        uint32_t t, d;
+        float pe;
+        check(ldsp_fmstereo_get_state(q, &t, &d, &pe));
+        return py::make_tuple(t, d, pe);
+    }
+    // complex64 IQ -> interleaved (L, R) float32
+    py::object call(const py::handle& x)
+    {
+        if (is_device_tensor(x)) {
+            DevIn d = dev_in(x, true);
+            size_t nout = 0;
+            check(ldsp_fmstereo_num_outputs(q, d.n, &nout));
+            py::object out = dev_empty(nout, false, d.device);
+            size_t nw = 0;
+            check(ldsp_fmstereo_execute(q, d.ptr, d.n, tptr(out), nout, &nw, LDSP_MEM_DEVICE, d.stream));
+            return out;
+        }
+        carr a = carr::ensure(x);
+        if (!a) throw py::error_already_set();
+        const size_t n = (size_t)a.size();
+        size_t nout = 0;
+        check(ldsp_fmstereo_num_outputs(q, n, &nout));
+        py::array_t<float> out(nout);
+        void* yp = out.mutable_data();
+        const void* xp = a.data();
+        size_t nw = 0;
+        int rc;
+        {
+            py::gil_scoped_release rel;
+            rc = ldsp_fmstereo_execute(q, xp, n, yp, nout, &nw, LDSP_MEM_HOST, nullptr);
+        }
+        check(rc);
+        return std::move(out);
+    }
+};
+
 // ------------------------------------------------------------------ Delay (utility.hpp:5-57)
 struct Delay {
     ldsp_delay_t q = nullptr;
@@ -951,6 +999,13 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("reset", &BroadcastAM::reset)
         .def_property("exact", &BroadcastAM::get_exact, &BroadcastAM::set_exact)
         .def("__call__", &BroadcastAM::call);
+
+    // ---- FMStereo (wrapper.cpp:264-267)
+    py::class_<FMStereo>(m, "FMStereo")
+        .def(py::init<float, float>(), py::arg("iq_rate") = 600000.0f, py::arg("pcm_rate") = 48000.0f)
+        .def("reset", &FMStereo::reset)
+        .def("state", &FMStereo::state)
+        .def("__call__", &FMStereo::call);
 
     // ---- RResampler / CResampler (wrapper.cpp:15-23)
     py::class_<RResampler>(m, "RResampler")

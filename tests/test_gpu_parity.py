@@ -48,16 +48,25 @@ def test_device_math_bitwise(ld, ora, rng):
         0: (np.float32(rng.uniform(-30, 30, n)), None),
         1: (np.float32(np.exp(rng.uniform(-80, 80, n))), None),
         2: (np.float32(rng.standard_normal(n)), np.float32(rng.standard_normal(n))),
+        5: None,   # atan2 special operands (zeros, infinities, NaN, tiny/huge ratios)
         3: (np.float32(rng.uniform(-12, 12, n)), None),
     }
     names = {0: "exp", 1: "log", 2: "atan2", 3: "tanh"}
-    for fn, (a, b) in cases.items():
+    sp = np.float32([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-38, -1e-38, 1e38, -1e38, 3e-45])
+    ga, gb = np.meshgrid(sp, sp)
+    cases[5] = (np.ascontiguousarray(ga.ravel()), np.ascontiguousarray(gb.ravel()))
+    for key, (a, b) in cases.items():
+        fn = 2 if key == 5 else key
         ta = torch.from_numpy(a).cuda()
         tb = torch.from_numpy(b if b is not None else a).cuda()
         ty = torch.empty_like(ta)
-        ld._math_eval(fn, ta.data_ptr(), tb.data_ptr(), ty.data_ptr(), n, 0)
+        ld._math_eval(fn, ta.data_ptr(), tb.data_ptr(), ty.data_ptr(), a.size, 0)
         torch.cuda.synchronize()
-        assert_bitwise(ty.cpu().numpy(), ora.math_eval(names[fn], a, b))
+        got, ref = ty.cpu().numpy(), ora.math_eval(names[fn], a, b)
+        if key == 5:                      # NaN payloads are not specified: NaN-ness only
+            assert np.array_equal(np.isnan(got), np.isnan(ref))
+            got, ref = got[~np.isnan(ref)], ref[~np.isnan(ref)]
+        assert_bitwise(got, ref)
     th = np.float32(rng.uniform(-20, 20, 4096))
     ta = torch.from_numpy(th).cuda()
     ty = torch.empty_like(ta)
@@ -459,6 +468,35 @@ def test_default_resamplers_bitwise(ld, ora, rng, rate):
     gr, orr = ld.RResampler(rate), ora.Resampler(rate, cplx=False, default=True)
     assert_bitwise(np.concatenate([gc(x[:999]), gc(x[999:])]), oc(x))
     assert_bitwise(np.concatenate([gr(r[:12345]), gr(r[12345:])]), orr(r))
+
+
+def _fm(rng, n, fs):
+    t = np.arange(n) / fs
+    left, right = np.sin(2 * np.pi * 1000 * t), 0.5 * np.sin(2 * np.pi * 3000 * t)
+    comp = 0.45 * (left + right) + 0.45 * (left - right) * np.cos(2 * np.pi * 38000 * t) \
+        + 0.1 * np.cos(2 * np.pi * 19000 * t)
+    x = np.exp(2j * np.pi * (75000 / fs) * np.cumsum(comp)) + 0.01 * cgauss(rng, n)
+    return x.astype(np.complex64)
+
+
+@pytest.mark.parametrize("iq_rate,pcm_rate", [(600000.0, 48000.0), (240000.0, 44100.0)])
+def test_fmstereo_bitwise(ld, ora, rng, iq_rate, pcm_rate):
+    x = _fm(rng, 150_000, iq_rate)
+    g, o = ld.FMStereo(iq_rate=iq_rate, pcm_rate=pcm_rate), ora.FMStereo(iq_rate, pcm_rate)
+    y = np.concatenate([g(x[:5000]), g(x[5000:5001]), g(x[5001:])])
+    assert_bitwise(y, o(x))
+    assert g.state() == o.state
+    g.reset()
+    o.reset()
+    assert_bitwise(g(x[:20_000]), o(x[:20_000]))
+
+
+def test_fmstereo_device_tensor(ld, ora, rng):
+    import torch
+    x = _fm(rng, 50_000, 600000.0)
+    y = ld.FMStereo()(torch.from_numpy(x).cuda())
+    assert y.is_cuda and y.dtype == torch.float32
+    assert_bitwise(y.cpu().numpy(), ora.FMStereo()(x))
 
 # ------------------------------------------------------------------ chain
 def _chain(ld, exact):
