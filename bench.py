@@ -107,6 +107,42 @@ def aggregate_value(world, n_per_rank, steps, elapsed):
     return world * n_per_rank * steps / elapsed / 1e6
 
 
+def scatter_channels(x_all, n, device):
+    """SURVEY 8(e) input scatter: rank 0 holds every channel's IQ block and
+    sends channel r to rank r with grouped point-to-point sends (RCCL has no
+    scatter primitive; over xGMI every peer has its own link).  Complex
+    blocks travel as their float32 (re, im) view.  Returns this rank's block."""
+    import torch.distributed as tdist
+    rank, world = tdist.get_rank(), tdist.get_world_size()
+    if rank == 0:
+        mine = x_all[0]
+        ops = [tdist.P2POp(tdist.isend, torch.view_as_real(x_all[r]), r) for r in range(1, world)]
+    else:
+        mine = torch.empty(n, dtype=torch.complex64, device=device)
+        ops = [tdist.P2POp(tdist.irecv, torch.view_as_real(mine), 0)]
+    if ops:
+        for req in tdist.batch_isend_irecv(ops):
+            req.wait()
+    return mine
+
+
+def gather_pcm(y):
+    """SURVEY 8(e) output gather: every rank's PCM block (same length on all
+    ranks: same rates, same block size) to rank 0.  Returns the list on rank 0."""
+    import torch.distributed as tdist
+    rank, world = tdist.get_rank(), tdist.get_world_size()
+    if rank != 0:
+        for req in tdist.batch_isend_irecv([tdist.P2POp(tdist.isend, y, 0)]):
+            req.wait()
+        return None
+    outs = [y] + [torch.empty_like(y) for _ in range(1, world)]
+    ops = [tdist.P2POp(tdist.irecv, outs[r], r) for r in range(1, world)]
+    if ops:
+        for req in tdist.batch_isend_irecv(ops):
+            req.wait()
+    return outs
+
+
 def cpu_baseline(n_iq, seconds=10.0):
     """Time the CPU restatement (oracle/, -O3, single thread) on a bounded sample."""
     from oracle import oracle as O
@@ -140,6 +176,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-components", action="store_true")
+    ap.add_argument("--scatter", action="store_true",
+                    help="rank 0 holds all channels: every step scatters the IQ blocks and gathers the PCM "
+                         "(SURVEY 8e) instead of each rank reading a resident channel")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,6 +195,9 @@ def main():
 
     import liquiddsp as L
     x = synth_channel(args.n, rank, device)
+    x_all = None
+    if args.scatter and dist and rank == 0:
+        x_all = torch.stack([x] + [synth_channel(args.n, r, device) for r in range(1, world)])
     radio = AMRadio(L)
     nst = len(radio.stages())
 
@@ -167,7 +209,10 @@ def main():
         if k == 0:
             L._profile_reset()                 # per-kernel HIP events over exactly the timed steps
             L._profile_enable(True)
-        out["y"] = radio(x, events[k] if k is not None else None)
+        xin = scatter_channels(x_all, args.n, device) if (args.scatter and dist) else x
+        out["y"] = radio(xin, events[k] if k is not None else None)
+        if args.scatter and dist:
+            gather_pcm(out["y"])
 
     elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize,
                           tdist.barrier if dist else (lambda: None))
@@ -216,7 +261,8 @@ def main():
         "config": {"workload": "AMRadio chain (cheby2 IIR ord8 -> resampler 48k/2M -> AGC -> AmpModem dsb+carrier "
                                "-> de-emphasis), one independent channel per GPU",
                    "samples_per_step_per_gpu": args.n, "iq_rate": 2000000, "pcm_rate": 48000,
-                   "pcm_samples_per_step": n_pcm, "parallelism": f"channel-per-gpu x{world}"},
+                   "pcm_samples_per_step": n_pcm,
+                   "parallelism": f"channel-per-gpu x{world}" + (" rank0-scatter/gather" if args.scatter and dist else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "ms_per_launch": round(dom_ms, 4),
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("bench", dom),
