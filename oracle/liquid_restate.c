@@ -676,6 +676,150 @@ static void cheby2_azpkf(unsigned int _n, float _es, float complex *_za, float c
     for (i = 0; i < 2 * L; i++) *_ka /= _za[i];
 }
 
+/* ---- elliptic prototype: liquid src/filter/src/ellip.c + iirdes.c ellip_azpkf,
+ * which follow S. J. Orfanidis, "Lecture notes on elliptic filter design"
+ * (Landen transformations; recalled, parity unpinned).  Analog pass-band
+ * edge 1 rad/s (fp = 1/2pi); the stop-band edge follows from the order. */
+#define ELLIP_NB 7
+static void landenf(float _k, unsigned int _n, float *_v)
+{
+    unsigned int i;
+    float k = _k;
+    for (i = 0; i < _n; i++) {
+        float kp = sqrtf(1.0f - k * k);
+        k = (k / (1.0f + kp)) * (k / (1.0f + kp));
+        _v[i] = k;
+    }
+}
+static void ellipkf(float _k, unsigned int _n, float *_K, float *_Kp)
+{
+    const float kmin = 4e-4f;
+    const float kmax = sqrtf(1.0f - kmin * kmin);
+    float kp = sqrtf(1.0f - _k * _k);
+    float v[ELLIP_NB], vp[ELLIP_NB];
+    unsigned int i;
+    float K, Kp;
+    if (_k > kmax) {
+        float L = -logf(0.25f * kp);
+        K = L + 0.25f * (L - 1.0f) * kp * kp;
+    } else {
+        landenf(_k, _n, v);
+        K = (float)M_PI * 0.5f;
+        for (i = 0; i < _n; i++) K *= (1.0f + v[i]);
+    }
+    if (kp > kmax) {
+        float L = -logf(0.25f * _k);
+        Kp = L + 0.25f * (L - 1.0f) * _k * _k;
+    } else {
+        landenf(kp, _n, vp);
+        Kp = (float)M_PI * 0.5f;
+        for (i = 0; i < _n; i++) Kp *= (1.0f + vp[i]);
+    }
+    *_K = K;
+    *_Kp = Kp;
+}
+static float ellipdegf(float _N, float _k1, unsigned int _n)
+{
+    float K1, K1p;
+    ellipkf(_k1, _n, &K1, &K1p);
+    float q1 = expf(-(float)M_PI * K1p / K1);
+    float q = powf(q1, 1.0f / _N);
+    float b = 0.0f, a = 0.0f;
+    unsigned int m;
+    for (m = 0; m <= _n; m++) b += powf(q, (float)(m * (m + 1)));
+    for (m = 1; m <= _n; m++) a += powf(q, (float)(m * m));
+    float g = b / (1.0f + 2.0f * a);
+    return 4.0f * sqrtf(q) * g * g;
+}
+/* cd(u K, k) and sn(u K, k) by descending Landen recursion */
+static float complex ellip_cdf(float complex _u, float _k, unsigned int _n)
+{
+    float v[ELLIP_NB];
+    landenf(_k, _n, v);
+    float complex w = ccosf(_u * (float)(M_PI * 0.5));
+    unsigned int i;
+    for (i = _n; i > 0; i--) w = (1.0f + v[i - 1]) * w / (1.0f + v[i - 1] * w * w);
+    return w;
+}
+static float complex ellip_snf(float complex _u, float _k, unsigned int _n)
+{
+    float v[ELLIP_NB];
+    landenf(_k, _n, v);
+    float complex w = csinf(_u * (float)(M_PI * 0.5));
+    unsigned int i;
+    for (i = _n; i > 0; i--) w = (1.0f + v[i - 1]) * w / (1.0f + v[i - 1] * w * w);
+    return w;
+}
+/* inverse cd / sn by ascending Landen recursion */
+static float complex ellip_acdf(float complex _w, float _k, unsigned int _n)
+{
+    float v[ELLIP_NB];
+    landenf(_k, _n, v);
+    float complex w = _w;
+    unsigned int i;
+    for (i = 0; i < _n; i++) {
+        float v1 = (i == 0) ? _k : v[i - 1];
+        w = w / (1.0f + csqrtf(1.0f - w * w * v1 * v1)) * 2.0f / (1.0f + v[i]);
+    }
+    return cacosf(w) * (float)(2.0 / M_PI);
+}
+static float complex ellip_asnf(float complex _w, float _k, unsigned int _n)
+{
+    return 1.0f - ellip_acdf(_w, _k, _n);
+}
+static void ellip_azpkf(unsigned int _n, float _ep, float _es, float complex *_za, float complex *_pa)
+{
+    const unsigned int nb = ELLIP_NB;
+    const float k1 = _ep / _es;
+    const float k = ellipdegf((float)_n, k1, nb);
+    const unsigned int r = _n % 2, L = (_n - r) / 2;
+    /* v0 = -j asn(j / ep, k1) / n (real) */
+    const float complex v0 = -_Complex_I * ellip_asnf(_Complex_I / _ep, k1, nb) / (float)_n;
+    unsigned int i, t = 0;
+    for (i = 0; i < L; i++) {
+        float ui = (2.0f * (i + 1) - 1.0f) / (float)_n;
+        float complex zeta = ellip_cdf(ui, k, nb);
+        _za[2 * i] = _Complex_I / (k * zeta);
+        _za[2 * i + 1] = conjf(_za[2 * i]);
+        float complex pz = _Complex_I * ellip_cdf(ui - _Complex_I * v0, k, nb);
+        _pa[t++] = pz;
+        _pa[t++] = conjf(pz);
+    }
+    if (r) _pa[t++] = crealf(_Complex_I * ellip_snf(_Complex_I * v0, k, nb));
+}
+
+/* ---- Bessel prototype: liquid iirdes.c bessel_azpkf (recalled, parity
+ * unpinned): poles = roots of the reverse Bessel polynomial
+ * theta_n(s) = sum_k (2n-k)! / (2^(n-k) k! (n-k)!) s^k (monic), here by
+ * Durand-Kerner in double precision, then divided by the approximate 3 dB
+ * frequency sqrt((2n-1) ln 2) [Bianchi 2007 (1.67)]. */
+static void bessel_azpkf(unsigned int _n, float complex *_pa)
+{
+    double c[65];
+    double complex z[64];
+    unsigned int i, j, it;
+    c[_n] = 1.0;                                  /* a_k / a_{k+1} = (2n-k)(k+1) / (2(n-k)) */
+    for (i = _n; i > 0; i--)
+        c[i - 1] = c[i] * (double)(2 * _n - (i - 1)) * (double)i / (2.0 * (double)(_n - (i - 1)));
+    const double rad = pow(c[0], 1.0 / _n);
+    for (i = 0; i < _n; i++) z[i] = rad * cpow(0.4 + 0.9 * I, (double)i);
+    for (it = 0; it < 1000; it++) {
+        double delta = 0.0;
+        for (i = 0; i < _n; i++) {
+            double complex val = 0.0, den = 1.0;
+            for (j = _n + 1; j > 0; j--) val = val * z[i] + c[j - 1];
+            for (j = 0; j < _n; j++)
+                if (j != i) den *= (z[i] - z[j]);
+            const double complex dz = val / den;
+            z[i] -= dz;
+            delta = fmax(delta, cabs(dz) / cabs(z[i]));
+        }
+        if (delta < 1e-16) break;
+    }
+    const float w3dB = sqrtf((2 * _n - 1) * logf(2.0f));
+    for (i = 0; i < _n; i++) _pa[i] = (float complex)z[i] / w3dB;
+}
+
 /* iirdes_freqprewarp */
 static float iirdes_freqprewarp(int _btype, float _fc, float _f0)
 {
@@ -884,9 +1028,25 @@ static int iirdes_dzpk_core(int _ftype, int _btype, unsigned int _n, float _fc, 
         k0 = 1.0f;
         cheby2_azpkf(_n, epsilon, za, pa, &ka);
         break;
+    case FT_ELLIP: {
+        nza = 2 * L;
+        float Gp = powf(10.0f, -_ap / 20.0f);
+        float Gs = powf(10.0f, -_as / 20.0f);
+        float ep = sqrtf(1.0f / (Gp * Gp) - 1.0f);
+        float es = sqrtf(1.0f / (Gs * Gs) - 1.0f);
+        k0 = r ? 1.0f : 1.0f / sqrtf(1.0f + ep * ep);
+        ellip_azpkf(_n, ep, es, za, pa);
+        (void)ka;
+        break;
+    }
+    case FT_BESSEL:
+        if (_n > 48) return -1;
+        nza = 0;
+        k0 = 1.0f;
+        bessel_azpkf(_n, pa);
+        break;
     default:
-        /* ellip / bessel: not restated */
-        return -2;
+        return -1;
     }
     float complex kd;
     float m = iirdes_freqprewarp(_btype, _fc, _f0);

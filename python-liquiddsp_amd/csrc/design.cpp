@@ -30,6 +30,8 @@ static constexpr double kPi = 3.14159265358979323846;
 // (1-ulp differences in the cheby2 poles / zeros).
 extern "C" void ldsp_cdivf(float ar, float ai, float br, float bi, float* out);
 extern "C" void ldsp_cdivd(double ar, double ai, double br, double bi, double* out);
+extern "C" void ldsp_ellip_azpkf(unsigned int n, float ep, float es, float* za, float* pa);
+extern "C" void ldsp_bessel_azpkf(unsigned int n, float* pa);
 static inline cf cdiv(cf x, cf y)
 {
     float r[2];
@@ -317,8 +319,22 @@ void dzpk(int ftype, int btype, unsigned int n, float fc, float f0, float ap, fl
         cheby2_azpk(n, es, za, pa);
         break;
     }
+    case 3: {   // elliptic (cplx_c.c)
+        const float Gp = powf(10.0f, -ap / 20.0f), Gs = powf(10.0f, -as / 20.0f);
+        const float ep = sqrtf(1.0f / (Gp * Gp) - 1.0f), es = sqrtf(1.0f / (Gs * Gs) - 1.0f);
+        k0 = cf(r ? 1.0f : 1.0f / sqrtf(1.0f + ep * ep), 0.0f);
+        za.assign(n - r, cf());
+        pa.assign(n, cf());
+        ldsp_ellip_azpkf(n, ep, es, reinterpret_cast<float*>(za.data()), reinterpret_cast<float*>(pa.data()));
+        break;
+    }
+    case 4:     // Bessel (cplx_c.c)
+        LDSP_REQUIRE(n <= 48, "iirdes: Bessel order must be <= 48");
+        pa.assign(n, cf());
+        ldsp_bessel_azpkf(n, reinterpret_cast<float*>(pa.data()));
+        break;
     default:
-        throw Error(LDSP_EUNSUP, "iirdes: elliptic and Bessel prototypes are not implemented");
+        throw Error(LDSP_EINVAL, "iirdes: unknown filter type");
     }
     bilinear(za, pa, k0, freqprewarp(btype, fc, f0), zd, pd, kd);
     if (btype == 1 || btype == 3) {

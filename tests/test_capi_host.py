@@ -118,7 +118,10 @@ def test_resampler_design_and_schedule(lib, ora, rate, m, fc, nf):
 
 PROTOS = [("butter", "lowpass", 4, 0.1, 0.0), ("cheby1", "lowpass", 5, 0.2, 0.0), ("cheby2", "lowpass", 8, 0.0075, 0.0),
           ("butter", "highpass", 6, 0.15, 0.0), ("cheby2", "highpass", 4, 0.05, 0.0),
-          ("butter", "bandpass", 3, 0.1, 0.25), ("cheby1", "bandstop", 2, 0.05, 0.2)]
+          ("butter", "bandpass", 3, 0.1, 0.25), ("cheby1", "bandstop", 2, 0.05, 0.2),
+          ("ellip", "lowpass", 4, 0.1, 0.0), ("ellip", "lowpass", 5, 0.2, 0.0), ("ellip", "highpass", 6, 0.05, 0.0),
+          ("ellip", "bandpass", 3, 0.1, 0.25), ("bessel", "lowpass", 4, 0.1, 0.0), ("bessel", "lowpass", 7, 0.02, 0.0),
+          ("bessel", "highpass", 3, 0.2, 0.0), ("bessel", "bandstop", 2, 0.05, 0.2)]
 FT = {"butter": 0, "cheby1": 1, "cheby2": 2, "ellip": 3, "bessel": 4}
 BT = {"lowpass": 0, "highpass": 1, "bandpass": 2, "bandstop": 3}
 
@@ -245,3 +248,29 @@ def test_module_calls_raise_without_gpu(ld):
         ld.ComplexResampler(rate=0.024, Fc=0.024)(np.zeros(100, np.complex64))
     with pytest.raises(RuntimeError):
         ld.AGC()(np.zeros(10, np.complex64))
+
+
+@pytest.mark.parametrize("ft", ["butter", "cheby1", "cheby2", "ellip", "bessel"])
+@pytest.mark.parametrize("bt", ["lowpass", "highpass", "bandpass", "bandstop"])
+def test_iir_freqresponse_all_types(lib, ft, bt):
+    """ldsp_iirfilt_freqresponse (iirfilter.hpp freqresponse -> iirfilt_*_freqresponse)
+    for every prototype / band type: |H| equals scipy's response of the same SOS."""
+    import scipy.signal as sps
+    q = C.c_void_p()
+    assert lib.ldsp_iirfilt_create_prototype(FT[ft], BT[bt], 4, C.c_float(0.08), C.c_float(0.2), C.c_float(1.0),
+                                             C.c_float(40.0), 1, C.byref(q)) == 0, lib.ldsp_last_error()
+    ns = C.c_uint()
+    lib.ldsp_iirfilt_get_nsos(q, C.byref(ns))
+    B = np.zeros(3 * ns.value, np.float32)
+    A = np.zeros(3 * ns.value, np.float32)
+    lib.ldsp_iirfilt_get_sos(q, ptr(B), ptr(A))
+    sos = np.hstack([B.reshape(-1, 3), A.reshape(-1, 3)]).astype(np.float64)
+    fs = np.linspace(0.0, 0.5, 41)
+    _, hr = sps.sosfreqz(sos, worN=fs, fs=1.0)
+    re_, im_ = C.c_float(), C.c_float()
+    got = []
+    for f in fs:
+        assert lib.ldsp_iirfilt_freqresponse(q, C.c_float(f), C.byref(re_), C.byref(im_)) == 0
+        got.append(complex(re_.value, im_.value))
+    assert np.max(np.abs(np.abs(got) - np.abs(hr))) < 1e-4
+    lib.ldsp_iirfilt_destroy(q)

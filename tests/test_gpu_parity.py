@@ -265,6 +265,24 @@ def test_iir_exact_bitwise(ld, ora, rng):
     assert_bitwise(y, o(x))
 
 
+@pytest.mark.parametrize("ft,bt,order,fc,f0", [("ellip", "lowpass", 6, 0.05, 0.3), ("ellip", "bandpass", 3, 0.05, 0.2),
+                                                 ("bessel", "lowpass", 5, 0.02, 0.3), ("bessel", "highpass", 4, 0.1, 0.3)])
+def test_iir_ellip_bessel(ld, ora, rng, ft, bt, order, fc, f0):
+    # the new prototypes through both IIR paths
+    x = cgauss(rng, 200_000)
+    o = ora.IIRFilter(prototype=(ft, bt, 1, order, np.float32(fc), f0, 0.7, 60.0))
+    g = ld.ComplexIIRFilter(filter_type=ft, band_type=bt, order=order, Fc=fc, F0=f0, Ap=0.7, As=60.0)
+    g.exact = True
+    assert_bitwise(np.concatenate([g(x[:777]), g(x[777:])]), o(x))
+    f = ld.ComplexIIRFilter(filter_type=ft, band_type=bt, order=order, Fc=fc, F0=f0, Ap=0.7, As=60.0)
+    o.reset()
+    truth = o.execute_f64(x)
+    o.reset()
+    # fast mode: float64 scan, or the exact speculative path for fast-decaying designs
+    err_gpu, err_liquid = maxrel(f(x), truth), maxrel(o(x), truth)
+    assert err_gpu <= max(err_liquid, 1e-6), (err_gpu, err_liquid)
+
+
 @pytest.mark.parametrize("n", [5000, 3 * 65536 + 17, 1 << 20, 1 << 26])
 def test_iir_fast_scan_accuracy(ld, ora, rng, n):
     x = cgauss(rng, n)

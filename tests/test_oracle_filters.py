@@ -311,3 +311,50 @@ def test_amradio_chain_runs_and_streams(ora, rng):
     assert np.array_equal(y.view(np.uint32), y2.view(np.uint32))
     assert len(y) == ((len(x) - 1) * (1 << 24) + 0xFFFFFF) // 699_050_688 + 1
     assert np.all(np.isfinite(y))
+
+
+# ---------------------------------------------------------------- elliptic / Bessel designs
+@pytest.mark.parametrize("order", [1, 2, 3, 4, 5, 6, 8])
+@pytest.mark.parametrize("btype", ["lowpass", "highpass"])
+def test_ellip_design_matches_scipy(ora, order, btype):
+    """The restated elliptic design (Orfanidis' Landen recursions in float32,
+    as liquid's ellip.c) against scipy.signal.ellip, whose analog prototype has
+    the same normalisation (pass-band edge 1 rad/s, order-determined stop-band
+    edge, DC gain 1 / sqrt(1 + ep^2) for even orders) and whose bilinear map
+    prewarps the same edge: the magnitude responses agree to float32 design
+    accuracy."""
+    import scipy.signal as sps
+    fc, Ap, As = 0.1, 1.0, 40.0
+    B, A = ora.iirdes("ellip", btype, order, fc, 0.0, Ap, As)
+    _, h = sps.sosfreqz(np.hstack([B, A]).astype(np.float64), worN=8192, fs=1.0)
+    _, hr = sps.sosfreqz(sps.ellip(order, Ap, As, 2 * fc, btype=btype, output="sos"), worN=8192, fs=1.0)
+    assert np.max(np.abs(np.abs(h) - np.abs(hr))) < 3e-4
+
+
+@pytest.mark.parametrize("order", [1, 2, 3, 4, 6, 9])
+def test_bessel_design_matches_scipy(ora, order):
+    """Bessel: the delay-normalised analog prototype (scipy norm='delay' =
+    roots of the reverse Bessel polynomial) scaled by 1 / sqrt((2n-1) ln 2),
+    bilinear with the prewarped cutoff."""
+    import scipy.signal as sps
+    fc = 0.1
+    B, A = ora.iirdes("bessel", "lowpass", order, fc, 0.0, 0.5, 60.0)
+    _, h = sps.sosfreqz(np.hstack([B, A]).astype(np.float64), worN=8192, fs=1.0)
+    z, p, k = sps.bessel(order, 1.0, analog=True, output="zpk", norm="delay")
+    p = p / np.sqrt((2 * order - 1) * np.log(2))
+    wc = 2 * np.tan(np.pi * fc)
+    zd, pd, kd = sps.bilinear_zpk(z, p * wc, np.real(np.prod(-p)) * wc ** order, fs=1.0)
+    _, hr = sps.sosfreqz(sps.zpk2sos(zd, pd, kd), worN=8192, fs=1.0)
+    assert np.max(np.abs(np.abs(h) - np.abs(hr))) < 1e-5
+
+
+@pytest.mark.parametrize("ft", ["ellip", "bessel"])
+@pytest.mark.parametrize("btype", ["bandpass", "bandstop"])
+def test_ellip_bessel_band_designs(ora, ft, btype):
+    """Band transforms of the new prototypes: unit peak gain, stable poles."""
+    import scipy.signal as sps
+    B, A = ora.iirdes(ft, btype, 4, 0.05, 0.2, 1.0, 40.0)
+    sos = np.hstack([B, A]).astype(np.float64)
+    _, h = sps.sosfreqz(sos, worN=8192, fs=1.0)
+    assert abs(np.max(np.abs(h)) - 1.0) < 1e-4
+    assert np.all(np.abs(np.roots(A[0])) < 1.0) and all(np.all(np.abs(np.roots(a)) < 1.0) for a in A)
