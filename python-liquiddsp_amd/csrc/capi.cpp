@@ -1465,13 +1465,16 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             // (k_agc.hip); measured on the AM chain at bandwidth 0.01 the exact loop then
             // coalesces within ~110 samples on average, 2834 at worst.
             const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
-            const int W = (int)std::min(1 << 18, std::max(512, (int)(20.0f / a)));
-            const int Wa = (int)std::min(1 << 20, std::max(2048, (int)(40.0f / a)));
+            static const float wmul = std::getenv("LDSP_AGC_WMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WMUL")) : 20.0f;
+            static const float wamul = std::getenv("LDSP_AGC_WAMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WAMUL")) : 40.0f;
+            static const int rounds = std::getenv("LDSP_AGC_ROUNDS") ? std::atoi(std::getenv("LDSP_AGC_ROUNDS")) : 3;
+            const int W = (int)std::min(1 << 18, std::max(256, (int)(wmul / a)));
+            const int Wa = (int)std::min(1 << 20, std::max(1024, (int)(wamul / a)));
             if (n >= (size_t)4 * (W + Wa)) {
                 k::SpecPlan p;
                 p.W = W;
                 p.Wa = Wa;
-                p.rounds = 3;
+                p.rounds = std::max(0, std::min(rounds, 6));
                 p.C = 256;
                 p.nchunks = (long)((n + p.C - 1) / p.C);
                 p.scratch = q->scratch.ensure(k::agc_scratch_bytes(p.nchunks), q->device);
@@ -1485,8 +1488,10 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
                     unsigned c[8];
                     LDSP_HIP(hipMemcpyAsync(c, p.dbg, sizeof(c), hipMemcpyDeviceToHost, e.stream));
                     LDSP_HIP(hipStreamSynchronize(e.stream));
-                    std::fprintf(stderr, "[ldsp agc] n=%zu chunks=%ld W=%d Wa=%d reruns: round0 %u round1 %u round2 %u verify %u\n",
-                                 n, p.nchunks, p.W, p.Wa, c[0], c[1], c[2], c[p.rounds]);
+                    std::fprintf(stderr, "[ldsp agc] n=%zu chunks=%ld W=%d Wa=%d rounds=%d reruns per round:", n, p.nchunks,
+                                 p.W, p.Wa, p.rounds);
+                    for (int r = 0; r <= p.rounds; r++) std::fprintf(stderr, " %u", c[r]);
+                    std::fprintf(stderr, " (last = verifier)\n");
                 }
             } else {
                 k::agc_seq(dx, n, q->dst.as<k::AgcState>(), dy, dstat, e.stream);

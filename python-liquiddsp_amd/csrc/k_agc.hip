@@ -7,10 +7,10 @@
 // sequential algorithm, but in parallel chunks: every chunk starts W samples
 // early from a guessed state (gain from the local input power), and because the
 // loop forgets its initial state the float32 trajectory coalesces bit-for-bit
-// with the true one well inside the warm-up (measured on the AM chain at
-// bandwidth 0.01: W = 4096 coalesces 50/51 chunks, 5120 all; W = 80/bandwidth).  A single-wave verifier checks each chunk's guessed start state against
-// its predecessor's end state and re-runs any chunk that did not coalesce, so
-// the output is always identical to the sequential evaluation.
+// with the true one inside the warm-up.  Chunks whose guessed start state
+// differs from the predecessor's end state are repaired run by run
+// (k_agc_runfix), and a single-wave verifier re-checks every chunk and re-runs
+// any leftover, so the output is always identical to the sequential evaluation.
 // (The AmpModem PLL lives in k_pll.hip.)
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
@@ -171,7 +171,7 @@ __global__ void k_agc_seq(const float2* __restrict__ x, long n, AgcState* st, fl
 // normalises the mean power of the kPow samples before it; that brings the
 // guess within a few ulps of the true trajectory, so the exact float32 loop
 // coalesces bit for bit within ~100 samples typically (a few thousand at
-// worst; chunks that have not are re-run by k_agc_fix / k_agc_verify).
+// worst; chunks that have not are re-run by k_agc_runfix / k_agc_verify).
 constexpr int kPow = 256;
 __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x, long n, const AgcState* st, int C,
                                                    int W, int Wa, long nch, unsigned* __restrict__ sc,
@@ -232,38 +232,56 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
     gs[7] = r.timer;
 }
 
-// Parallel repair round: every chunk of the given parity whose start state
-// differs from its predecessor's end state re-runs from that end state
-// (in place; the predecessors have the other parity, so nothing they hold
-// changes during the launch).  Chunks that start from the true state
-// (s0 <= W) are exact already.
-__global__ void __launch_bounds__(64) k_agc_fix(const float2* __restrict__ x, long n, const AgcState* st, int C,
-                                                int W, long nch, int parity, unsigned* __restrict__ sc,
-                                                float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg)
+// Parallel repair round over runs of failed chunks.  flags (k_agc_flags)
+// mark the chunks whose guessed start state differs from the predecessor's
+// end state; one thread per run start (flagged chunk with an unflagged
+// predecessor, whose end state is the true one) re-runs the whole run in
+// order from that end state, then keeps going through unflagged chunks until
+// its state equals a chunk's stored start state bit for bit (from there the
+// stored chunks are the true trajectory).  It stops early at the next run's
+// start, whose own thread began from a stale state: the next flags pass
+// catches that.  One round replaces the ~R/2 parity rounds a run of R failed
+// chunks needed.
+__device__ __forceinline__ bool agc_flag(const unsigned long long* flags, long c)
 {
-    const long chunk = ((long)blockIdx.x * 64 + threadIdx.x) * 2 + parity;
-    if (chunk < 1 || chunk >= nch || chunk * C - W <= 0) return;
-    unsigned* gs = sc + chunk * 8;
-    const unsigned* pe = sc + (chunk - 1) * 8 + 4;
-    unsigned e[4];
-    bool same = true;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        e[i] = pe[i];
-        same &= e[i] == gs[i];
-    }
-    if (same) return;
-    if (dbg) atomicAdd(dbg, 1u);
+    return (flags[c >> 6] >> (c & 63)) & 1ull;
+}
+
+__global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x, long n, const AgcState* st, int C,
+                                                   long nch, unsigned* __restrict__ sc,
+                                                   const unsigned long long* __restrict__ flags,
+                                                   float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg)
+{
+    const long k = (long)blockIdx.x * 64 + threadIdx.x;
+    if (k < 1 || k >= nch || !agc_flag(flags, k) || agc_flag(flags, k - 1)) return;
     const AgcState p = *st;
-    AgcReg r{__uint_as_float(e[0]), __uint_as_float(e[1]), (int)e[2], e[3]};
-    const long s0 = chunk * C;
-    agc_run<true>(r, p, x, s0, min(n, s0 + C), y, status);
-#pragma unroll
-    for (int i = 0; i < 4; i++) gs[i] = e[i];
-    gs[4] = __float_as_uint(r.g);
-    gs[5] = __float_as_uint(r.y2p);
-    gs[6] = (unsigned)r.mode;
-    gs[7] = r.timer;
+    const unsigned* pe = sc + (k - 1) * 8 + 4;
+    AgcReg r{__uint_as_float(ldntu(pe)), __uint_as_float(ldntu(pe + 1)), (int)ldntu(pe + 2), ldntu(pe + 3)};
+    bool inrun = true;
+    for (long m = k; m < nch; m++) {
+        unsigned* gs = sc + m * 8;
+        if (m > k) {
+            const bool b = agc_flag(flags, m);
+            if (!(inrun && b)) {
+                if (b) break;                               // the next run's start
+                inrun = false;
+                if (ldntu(gs) == __float_as_uint(r.g) && ldntu(gs + 1) == __float_as_uint(r.y2p) &&
+                    ldntu(gs + 2) == (unsigned)r.mode && ldntu(gs + 3) == r.timer)
+                    break;                                  // coalesced with the stored trajectory
+            }
+        }
+        if (dbg) atomicAdd(dbg, 1u);
+        gs[0] = __float_as_uint(r.g);
+        gs[1] = __float_as_uint(r.y2p);
+        gs[2] = (unsigned)r.mode;
+        gs[3] = r.timer;
+        const long s0 = m * C;
+        agc_run<true>(r, p, x, s0, min(n, s0 + C), y, status);
+        gs[4] = __float_as_uint(r.g);
+        gs[5] = __float_as_uint(r.y2p);
+        gs[6] = (unsigned)r.mode;
+        gs[7] = r.timer;
+    }
 }
 
 // Parallel pre-check: bit c of flags[c / 64] = chunk c's start state differs
@@ -386,21 +404,24 @@ void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y,
                            status);
     }
     LDSP_HIP(hipGetLastError());
-    for (int round = 0; round < p.rounds; round++)
-        for (int parity = 1; parity >= 0; parity--) {
-            LDSP_PROF(s, "k_agc_fix");
-            hipLaunchKernelGGL(k_agc_fix, dim3((unsigned)((p.nchunks / 2 + 64) / 64)), dim3(64), 0, s,
-                               (const float2*)x, (long)n, (const AgcState*)st, p.C, p.W, p.nchunks, parity,
-                               (unsigned*)p.scratch, (float2*)y, status, p.dbg ? p.dbg + round : nullptr);
-        }
-    LDSP_HIP(hipGetLastError());
     unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
-    {
-        LDSP_PROF(s, "k_agc_flags");
-        hipLaunchKernelGGL(k_agc_flags, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, p.C, p.W, p.nchunks,
-                           (const unsigned*)p.scratch, flags);
+    const unsigned nb = (unsigned)((p.nchunks + 63) / 64);
+    for (int round = 0; round <= p.rounds; round++) {
+        {
+            LDSP_PROF(s, "k_agc_flags");
+            hipLaunchKernelGGL(k_agc_flags, dim3(nb), dim3(64), 0, s, p.C, p.W, p.nchunks, (const unsigned*)p.scratch,
+                               flags);
+        }
+        LDSP_HIP(hipGetLastError());
+        if (round == p.rounds) break;
+        {
+            LDSP_PROF(s, "k_agc_runfix");
+            hipLaunchKernelGGL(k_agc_runfix, dim3(nb), dim3(64), 0, s, (const float2*)x, (long)n,
+                               (const AgcState*)st, p.C, p.nchunks, (unsigned*)p.scratch,
+                               (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr);
+        }
+        LDSP_HIP(hipGetLastError());
     }
-    LDSP_HIP(hipGetLastError());
     {
         LDSP_PROF(s, "k_agc_verify");
         hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, p.nchunks,

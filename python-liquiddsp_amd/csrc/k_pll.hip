@@ -647,6 +647,8 @@ void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_ou
         LDSP_HIP(hipGetLastError());
         {
             LDSP_PROF(s, "k_pll_walk");
+            // (a variant deciding the repair direction on the scalar unit, s_cselect over four
+            // readlanes and mask-selected output patches, measured 12 % slower: 5.85 vs 5.21 ms)
             if (alpha_host <= 1.0f / 512.0f)
                 hipLaunchKernelGGL(k_pll_walk<true>, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
             else
