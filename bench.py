@@ -170,12 +170,16 @@ def cpu_baseline(n_iq, seconds=10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-components", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the steps rotate over (1 = every step on torch's current stream). "
+                         "Each object orders its own calls across streams (libldsp StreamMark), so step k+1's "
+                         "IIR/resampler/AGC/candidate kernels overlap step k's serial PLL walk")
     ap.add_argument("--scatter", action="store_true",
                     help="rank 0 holds all channels: every step scatters the IQ blocks and gathers the PCM "
                          "(SURVEY 8e) instead of each rank reading a resident channel")
@@ -205,21 +209,29 @@ def main():
               for _ in range(args.steps)]
     out = {}
 
-    def step(k):
-        if k == 0:
+    nstreams = 1 if (args.scatter and dist) else max(1, args.streams)
+    streams = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(nstreams - 1)]
+    barrier = tdist.barrier if dist else (lambda: None)
+
+    def step(k, prof=True, rot=nstreams):
+        if k == 0 and prof:
             L._profile_reset()                 # per-kernel HIP events over exactly the timed steps
             L._profile_enable(True)
         xin = scatter_channels(x_all, args.n, device) if (args.scatter and dist) else x
-        out["y"] = radio(xin, events[k] if k is not None else None)
+        with torch.cuda.stream(streams[(k or 0) % rot]):
+            out["y"] = radio(xin, events[k] if (k is not None and prof) else None)
         if args.scatter and dist:
             gather_pcm(out["y"])
 
-    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize,
-                          tdist.barrier if dist else (lambda: None))
+    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, barrier)
     L._profile_enable(False)
     kprof = L._profile_report()
+    # the same chain with every step on one stream (no overlap between steps), for reference
+    single = timed_steps(lambda k: step(k, prof=False, rot=1), min(args.steps, 5), 1, torch.cuda.synchronize, barrier)
+    single_steps = min(args.steps, 5)
     if dist:
         elapsed = reduce_max(elapsed, device)
+        single = reduce_max(single, device)
     y = out["y"]
 
     stage_ms = {name: float(np.mean([events[k][i][0].elapsed_time(events[k][i][1]) for k in range(args.steps)]))
@@ -269,6 +281,8 @@ def main():
                      "traffic_source": PMC_SOURCE,
                      "note": "alg bytes = 12 B per PCM sample (AmpModem in + out); the PLL recurrence is "
                              "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else ""},
+        "streams": nstreams,
+        "single_stream_ms_per_step": round(single / single_steps * 1e3, 4),
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "kernels": kernels,
     }

@@ -118,6 +118,7 @@ struct FirObj {
     bool fft_ready = false;
     int cur = 0;
     hipStream_t last = nullptr;
+    StreamMark ord;                   // cross-stream call order (ldsp_common.hpp)
     Staging stg;
     size_t esz() const { return cplx ? 8 : 4; }
     // FAST on complex data with L in [kFirFftMinTaps, 1025] runs the overlap-save
@@ -206,6 +207,7 @@ struct ResampObj {
     DevBuf dsub, hist[2];
     int cur = 0;
     hipStream_t last = nullptr;
+    StreamMark ord;                   // cross-stream call order (ldsp_common.hpp)
     Staging stg;
     size_t esz() const { return cplx ? 8 : 4; }
     void set_rate(float r)
@@ -286,6 +288,7 @@ struct IirObj {
     long plan_nch = 0;
     int plan_G = 0;
     hipStream_t last = nullptr;
+    StreamMark ord;                   // cross-stream call order (ldsp_common.hpp)
     Staging stg;
     std::vector<double> A;            // D x D one-step state matrix (float64)
 
@@ -508,6 +511,7 @@ struct AgcObj {
     bool dev_newer = false;           // device state advanced past the mirror
     bool upload_pending = true;
     hipStream_t last = nullptr;
+    StreamMark ord;                   // cross-stream call order (ldsp_common.hpp)
     Staging stg;
     void init()
     {
@@ -552,10 +556,20 @@ struct AmpObj {
     std::vector<float> lp, dc, table;
     k::AmpState st{};
     int device = -1;
-    DevBuf dlp, ddc, dtab, dst, lph[2], dch[2], dlh[2], x0, mb, pll;
+    DevBuf dlp, ddc, dtab, dst, lph[2], dch[2];
+    // Per-call scratch in two slots (call parity) and the delay-line history in
+    // three (call index mod 3), so that call k's front half (lowpass, history,
+    // candidates) can run while call k-1's walker still reads its own slot.
+    DevBuf x0[2], mb[2], pll[2], dlh[3];
+    unsigned long long ncall = 0;
     int cur = 0;
     bool dev_newer = false;
     hipStream_t last = nullptr;
+    // Cross-stream order (ldsp_common.hpp): `front` = end of a call's front half
+    // (lowpass + delay histories, candidate guess state), `ord` = end of a call
+    // (true PLL state, DC-blocker history), `slot[i]` = end of the last call that
+    // used scratch slot i.
+    StreamMark front, ord, slot[2];
     Staging stg;
     void reset_host()
     {
@@ -563,6 +577,16 @@ struct AmpObj {
         st.dtheta = 0;
         st.alpha = 0.001f;
         st.beta = sqrtf(st.alpha);
+        for (int i = 0; i < 2; i++) {
+            st.gth[i] = st.theta;
+            st.gd[i] = st.dtheta;
+        }
+    }
+    void sync_all()
+    {
+        ord.sync();
+        front.sync();
+        for (auto& sm : slot) sm.sync();
     }
     void ensure_device()
     {
@@ -579,8 +603,10 @@ struct AmpObj {
             zero_now(lph[i].p, 0, (2 * m) * 8);
             dch[i].ensure((2 * m) * 4, dev);
             zero_now(dch[i].p, 0, (2 * m) * 4);
-            dlh[i].ensure(m * 8, dev);
-            zero_now(dlh[i].p, 0, m * 8);
+        }
+        for (auto& b : dlh) {
+            b.ensure(m * 8, dev);
+            zero_now(b.p, 0, m * 8);
         }
         device = dev;
     }
@@ -607,6 +633,7 @@ struct ldsp_freqdem_s {
     int device = -1, cur = 0;
     ldsp::DevBuf prev[2];
     hipStream_t last = nullptr;
+    ldsp::StreamMark ord;                   // cross-stream call order (ldsp_common.hpp)
     ldsp::Staging stg;
 };
 
@@ -622,6 +649,7 @@ struct ldsp_fmstereo_s {
     int device = -1;
     ldsp::DevBuf dst, dtab, sbuf, lr[2], le[2], out[2];
     hipStream_t last = nullptr;
+    ldsp::StreamMark ord;                  // cross-stream call order (ldsp_common.hpp)
     ldsp::Staging stg;
 };
 
@@ -630,6 +658,7 @@ struct ldsp_delay_s {
     int device = -1, cr = 0, cc = 0;
     ldsp::DevBuf hr[2], hc[2];     // real / complex lines of nd + 1 samples
     hipStream_t last = nullptr;
+    ldsp::StreamMark ord;                  // cross-stream call order (ldsp_common.hpp)
     ldsp::Staging stg;
     void zero()
     {
@@ -893,6 +922,7 @@ int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int
         q->ensure_device();
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
+        q->ord.wait(e.stream);
         const size_t bytes = n * q->esz();
         const void* dx = q->stg.dev_in(e, x, bytes);
         void* dy = q->stg.dev_out(e, y, bytes);
@@ -912,6 +942,7 @@ int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int
                 k::fir_fast(q->cplx, dx, hin, hout, n, q->taps_pad.as<float>(), L, q->scale, dy, e.stream);
             if (L > 1) q->cur = 1 - q->cur;
         }
+        q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, bytes);
     });
@@ -1023,6 +1054,7 @@ int ldsp_resamp_execute(ldsp_resamp_t q, const void* x, size_t n, void* y, size_
         q->ensure_device();
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
+        q->ord.wait(e.stream);
         const void* dx = q->stg.dev_in(e, x, n * q->esz());
         void* dy = q->stg.dev_out(e, y, K * q->esz());
         if (n > 0) {
@@ -1045,6 +1077,7 @@ int ldsp_resamp_execute(ldsp_resamp_t q, const void* x, size_t n, void* y, size_
             if (q->sub_len > 1) q->cur = 1 - q->cur;
             q->phase = (uint64_t)((long long)q->phase + (long long)K * q->step - (long long)n * (1LL << 24));
         }
+        q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, K * q->esz());
     });
@@ -1284,6 +1317,7 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
         q->ensure_device();
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
+        q->ord.wait(e.stream);
         const size_t bytes = n * (q->cplx ? 8 : 4);
         const void* dx = q->stg.dev_in(e, x, bytes);
         void* dy = q->stg.dev_out(e, y, bytes);
@@ -1312,6 +1346,7 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
                 k::iir_scan(q->cplx, d, dx, n, q->st64.as<double>(), p, dy, e.stream);
             }
         }
+        q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, bytes);
     });
@@ -1452,6 +1487,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         q->ensure_device();
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
+        q->ord.wait(e.stream);
         if (q->upload_pending) {
             LDSP_HIP(hipStreamSynchronize(e.stream));
             LDSP_HIP(hipMemcpy(q->dst.p, &q->h, sizeof(q->h), hipMemcpyHostToDevice));
@@ -1498,6 +1534,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             }
             q->dev_newer = true;
         }
+        q->ord.mark(e.stream);
         q->last = e.stream;
         if (status && n > 0) {
             LDSP_HIP(hipMemcpyAsync(status, dstat, n, hipMemcpyDeviceToHost, e.stream));
@@ -1539,12 +1576,14 @@ static void amp_reset(AmpObj* q)
     q->dev_newer = false;
     if (q->device < 0) return;
     DeviceGuard g(q->device);
-    if (q->last) LDSP_HIP(hipStreamSynchronize(q->last));
+    q->sync_all();
     LDSP_HIP(hipMemcpy(q->dst.p, &q->st, sizeof(q->st), hipMemcpyHostToDevice));
     for (int i = 0; i < 2; i++) {
-        for (DevBuf* b : {&q->lph[i], &q->dch[i], &q->dlh[i]})
+        for (DevBuf* b : {&q->lph[i], &q->dch[i]})
             if (b->p) zero_now(b->p, 0, b->cap);
     }
+    for (auto& b : q->dlh)
+        if (b.p) zero_now(b.p, 0, b.cap);
 }
 int ldsp_ampmodem_reset(ldsp_ampmodem_t q)
 {
@@ -1559,7 +1598,7 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
         NONNULL(q);
         if (q->dev_newer) {
             DeviceGuard g(q->device);
-            LDSP_HIP(hipStreamSynchronize(q->last));
+            q->sync_all();
             LDSP_HIP(hipMemcpy(&q->st, q->dst.p, sizeof(q->st), hipMemcpyDeviceToHost));
             q->dev_newer = false;
         }
@@ -1569,23 +1608,61 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
 }
 
 // Carrier lowpass + delay + PLL walk of AmpModem / BroadcastAM: writes
-// re(v1) / mod_index (costas 0) or the Costas-loop output (costas 1) to mbuf.
-static void amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, float mod_index, int costas, float* mbuf)
+// re(v1) / mod_index (costas 0) or the Costas-loop output (costas 1) to mbuf
+// (slot scratch when mbuf is null).  Returns the buffer written.  The caller
+// enqueues its post-filter and then amp_call_end().  Stream order (see AmpObj):
+//   wait slot[s] (call k-2 done with slot s) and front (call k-1's histories and guess)
+//   lowpass, delay history, candidates            -> mark front
+//   wait ord (call k-1's walk and DC blocker)      -> walker
+static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, float mod_index, int costas, float* mbuf)
 {
     const int L = 2 * (int)q->m + 1;
-    void* x0 = q->x0.ensure(n * 8, q->device);
+    const int sl = (int)(q->ncall & 1);
+    const int h3 = (int)(q->ncall % 3);
+    q->slot[sl].wait(e.stream);
+    q->front.wait(e.stream);
+    if (!mbuf) mbuf = (float*)q->mb[sl].ensure(n * 4, q->device);
+    void* x0 = q->x0[sl].ensure(n * 8, q->device);
     k::fir_exact(true, dx, q->lph[q->cur].p, q->lph[1 - q->cur].p, n, q->dlp.as<float>(), L, 1.0f, x0, e.stream);
-    void* pscr = q->pll.ensure(k::pll_scratch_bytes(n), q->device);
-    k::ampmodem_pll(x0, dx, q->dlh[q->cur].p, q->dlh[1 - q->cur].p, (int)q->m, n, q->dst.as<k::AmpState>(),
-                    q->dtab.as<float>(), mod_index, costas, q->st.alpha, mbuf, pscr, e.stream);
-    if (n >= 8192 && std::getenv("LDSP_DEBUG_PLL")) {
+    k::PllCall c;
+    c.x0 = x0;
+    c.x = dx;
+    c.hist = q->dlh[h3].p;
+    c.hist_out = q->dlh[(h3 + 1) % 3].p;
+    c.m = (int)q->m;
+    c.n = n;
+    c.st = q->dst.as<k::AmpState>();
+    c.gcur = (int)(q->ncall & 1);
+    c.table = q->dtab.as<float>();
+    c.mod_index = mod_index;
+    c.costas = costas;
+    c.alpha_host = q->st.alpha;
+    c.y = mbuf;
+    c.scratch = k::pll_parallel(n) ? q->pll[sl].ensure(k::pll_scratch_bytes(n), q->device) : nullptr;
+    k::pll_front(c, e.stream);
+    const bool par = k::pll_parallel(n);
+    if (par) q->front.mark(e.stream);     // the sequential loop writes the guess itself: mark after it
+    q->ord.wait(e.stream);
+    k::pll_back(c, e.stream);
+    if (!par) q->front.mark(e.stream);
+    if (par && std::getenv("LDSP_DEBUG_PLL")) {
         unsigned long long stt[4];
-        LDSP_HIP(hipMemcpyAsync(stt, (char*)pscr + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
+        LDSP_HIP(hipMemcpyAsync(stt, (char*)c.scratch + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
                                 e.stream));
         LDSP_HIP(hipStreamSynchronize(e.stream));
         std::fprintf(stderr, "[ldsp pll] n=%zu repairs=%llu unused=%llu walk_clk=%llu wait_clk=%llu\n", n, stt[0],
                      stt[1], stt[2], stt[3]);
     }
+    return mbuf;
+}
+
+static void amp_call_end(AmpObj* q, const Exec& e)
+{
+    q->ord.mark(e.stream);
+    q->slot[q->ncall & 1].mark(e.stream);
+    q->ncall++;
+    q->cur = 1 - q->cur;
+    q->dev_newer = true;
 }
 
 int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y, int mem, void* stream)
@@ -1600,13 +1677,11 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
         if (n > 0) {
             const int L = 2 * (int)q->m + 1;
-            float* mbuf = q->suppressed ? dy : (float*)q->mb.ensure(n * 4, q->device);
-            amp_pll_stage(q, e, dx, n, q->mod_index, q->suppressed ? 1 : 0, mbuf);
+            float* mbuf = amp_pll_stage(q, e, dx, n, q->mod_index, q->suppressed ? 1 : 0, q->suppressed ? dy : nullptr);
             if (!q->suppressed)
                 k::fir_exact(false, mbuf, q->dch[q->cur].p, q->dch[1 - q->cur].p, n, q->ddc.as<float>(), L, 1.0f,
                              dy, e.stream);
-            q->cur = 1 - q->cur;
-            q->dev_newer = true;
+            amp_call_end(q, e);
         }
         q->last = e.stream;
         q->stg.finish(e, y, n * 4);
@@ -1678,16 +1753,14 @@ int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void* x, size_t n, void* y, 
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
         if (n > 0) {
-            float* mbuf = (float*)q->mb.ensure(n * 4, q->device);
-            amp_pll_stage(q, e, dx, n, 1.0f, 0, mbuf);
+            float* mbuf = amp_pll_stage(q, e, dx, n, 1.0f, 0, nullptr);
             const int rc = ldsp_iirfilt_execute(q->dcb, mbuf, n, dy, LDSP_MEM_DEVICE, e.stream);
             if (rc != LDSP_OK) throw Error(rc, g_last_error);
             if (pre) {
                 LDSP_HIP(hipMemcpyAsync(pre, mbuf, n * 4, e.host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice,
                                         e.stream));
             }
-            q->cur = 1 - q->cur;
-            q->dev_newer = true;
+            amp_call_end(q, e);
         }
         q->last = e.stream;
         q->stg.finish(e, y, n * 4);
@@ -1743,12 +1816,14 @@ int ldsp_freqdem_demodulate(ldsp_freqdem_t q, const void* x, size_t n, void* y, 
         }
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
+        q->ord.wait(e.stream);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
         if (n > 0) {
             k::freqdem(dx, q->prev[q->cur].p, q->prev[1 - q->cur].p, n, q->ref, dy, e.stream);
             q->cur = 1 - q->cur;
         }
+        q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, n * 4);
     });
@@ -1804,6 +1879,7 @@ int ldsp_delay_execute(ldsp_delay_t q, const void* x, size_t n, int cplx, void* 
         }
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
+        q->ord.wait(e.stream);
         const size_t es = cplx ? 8 : 4;
         const void* dx = q->stg.dev_in(e, x, n * es);
         void* dy = q->stg.dev_out(e, y, n * es);
@@ -1814,6 +1890,7 @@ int ldsp_delay_execute(ldsp_delay_t q, const void* x, size_t n, int cplx, void* 
             k::delay(cplx != 0, dx, h[c].p, h[1 - c].p, n, D, dy, e.stream);
             c = 1 - c;
         }
+        q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, n * es);
     });
@@ -1924,6 +2001,7 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
         }
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
+        q->ord.wait(e.stream);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, 2 * k * 4);
         if (n > 0) {
@@ -1946,6 +2024,7 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
             }
             k::interleave2(outs[0], outs[1], k, dy, e.stream);
         }
+        q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, 2 * k * 4);
     });

@@ -84,7 +84,7 @@ __device__ __forceinline__ Kick pll_eval(const float* tab, uint32_t i, float2 u0
 // ------------------------------------------------------------------ sequential
 constexpr int kSeqChunk = 2048;
 
-__global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st, float* __restrict__ y)
+__global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st, int gcur, float* __restrict__ y)
 {
     __shared__ float tab[1024];
     __shared__ float2 b0[kSeqChunk], b1[kSeqChunk];
@@ -112,6 +112,8 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
     if (tid == 0) {
         st->theta = theta;
         st->dtheta = d;
+        st->gth[1 - gcur] = theta;     // exact: the next call's candidates start on the true state
+        st->gd[1 - gcur] = d;
     }
 }
 
@@ -187,7 +189,12 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
     }
 }
 
-__global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpState* st, long nchc, CandBuf cb,
+// Candidate chunk k starts `warm` samples early from the guess state (the
+// previous call's last candidate end state, or the true state after a reset or a
+// sequential call), extrapolated at constant frequency.  The guess is never the
+// true state of a walk still in progress, so this kernel can overlap the
+// previous call's walker; the walker carries the exact offset either way.
+__global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st, int gcur, long nchc, CandBuf cb,
                                                  float* __restrict__ y, int warm)
 {
     __shared__ float tab[1024];
@@ -197,12 +204,14 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpStat
     if (k >= nchc) return;
     const long s0 = k * kCand, s1 = min(n, s0 + kCand);
     const float alpha = st->alpha, beta = st->beta;
-    uint32_t theta = st->theta, d = st->dtheta;
+    const uint32_t g_th = st->gth[gcur];
+    uint32_t d = st->gd[gcur];
+    uint32_t theta = g_th;
     long w0 = s0 - warm;
     if (w0 <= 0) {
-        w0 = 0;                                       // exact: from the true state
+        w0 = 0;
     } else {
-        theta = st->theta + (uint32_t)((uint64_t)w0 * d);   // constant-frequency extrapolation
+        theta = g_th + (uint32_t)((uint64_t)w0 * d);   // constant-frequency extrapolation
     }
     cand_run<false>(in, tab, w0, s0, alpha, beta, theta, d, cb, y);
     cb.cs[2 * k] = theta;
@@ -210,6 +219,10 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, const AmpStat
     cand_run<true>(in, tab, s0, s1, alpha, beta, theta, d, cb, y);
     cb.ce[2 * k] = theta;
     cb.ce[2 * k + 1] = d;
+    if (k == nchc - 1) {                 // guess for the next call (other slot: every thread read [gcur])
+        st->gth[1 - gcur] = theta;
+        st->gd[1 - gcur] = d;
+    }
 }
 
 // ------------------------------------------------------------------ walker
@@ -607,60 +620,79 @@ size_t pll_stats_offset(size_t n)
     return nblk * kBlk * 32 + nblk * kSub * 16;
 }
 
-void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_out, int m, size_t n, AmpState* st,
-                  const float* table, float mod_index, int costas, float alpha_host, float* y, void* scratch,
-                  hipStream_t s)
+bool pll_parallel(size_t n) { return n >= (size_t)4 * kWarm; }
+
+static PllIn pll_in(const PllCall& c)
 {
-    if (n == 0) return;
     PllIn in;
-    in.x0 = (const float2*)x0;
-    in.x = (const float2*)x;
-    in.hist = (const float2*)hist;
-    in.m = m;
-    in.table = table;
-    in.mod_index = mod_index;
-    in.costas = costas;
-    if (n < (size_t)4 * kWarm || scratch == nullptr) {
-        {
-            LDSP_PROF(s, "k_pll_seq");
-            hipLaunchKernelGGL(k_pll_seq, dim3(1), dim3(256), 0, s, in, (long)n, st, y);
-        }
-        LDSP_HIP(hipGetLastError());
-    } else {
-        const long nblk = (long)((n + kBlk - 1) / kBlk);
-        const long nchc = (long)((n + kCand - 1) / kCand);
-        CandBuf cb;
-        cb.npad = nblk * kBlk;
-        char* p = (char*)scratch;
-        cb.rec = (uint4*)p;
-        cb.cs = (uint32_t*)(p + (size_t)cb.npad * 32);
-        cb.ce = cb.cs + 2 * nblk * kSub;
-        cb.stats = (unsigned long long*)(p + pll_stats_offset(n));
-        static const int dbg_mode = std::getenv("LDSP_DEBUG_PLL_MODE") ? std::atoi(std::getenv("LDSP_DEBUG_PLL_MODE")) : 0;
-        cb.dbg = dbg_mode;
-        {
-            LDSP_PROF(s, "k_pll_cand");
-            static const int warm = std::getenv("LDSP_PLL_WARM") ? std::atoi(std::getenv("LDSP_PLL_WARM")) : kWarm;
-            hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((nchc + 63) / 64)), dim3(64), 0, s, in, (long)n,
-                               (const AmpState*)st, nchc, cb, y, warm);
-        }
-        LDSP_HIP(hipGetLastError());
-        {
-            LDSP_PROF(s, "k_pll_walk");
-            // (a variant deciding the repair direction on the scalar unit, s_cselect over four
-            // readlanes and mask-selected output patches, measured 12 % slower: 5.85 vs 5.21 ms)
-            if (alpha_host <= 1.0f / 512.0f)
-                hipLaunchKernelGGL(k_pll_walk<true>, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
-            else
-                hipLaunchKernelGGL(k_pll_walk<false>, dim3(1), dim3(kWalkThreads), 0, s, in, (long)n, st, nblk, cb, y);
-        }
-        LDSP_HIP(hipGetLastError());
-    }
-    // delay-line history for the next call (m samples); k_pll_* read the old one
+    in.x0 = (const float2*)c.x0;
+    in.x = (const float2*)c.x;
+    in.hist = (const float2*)c.hist;
+    in.m = c.m;
+    in.table = c.table;
+    in.mod_index = c.mod_index;
+    in.costas = c.costas;
+    return in;
+}
+
+static CandBuf cand_buf(const PllCall& c)
+{
+    const long nblk = (long)((c.n + kBlk - 1) / kBlk);
+    CandBuf cb;
+    cb.npad = nblk * kBlk;
+    char* p = (char*)c.scratch;
+    cb.rec = (uint4*)p;
+    cb.cs = (uint32_t*)(p + (size_t)cb.npad * 32);
+    cb.ce = cb.cs + 2 * nblk * kSub;
+    cb.stats = (unsigned long long*)(p + pll_stats_offset(c.n));
+    static const int dbg_mode = std::getenv("LDSP_DEBUG_PLL_MODE") ? std::atoi(std::getenv("LDSP_DEBUG_PLL_MODE")) : 0;
+    cb.dbg = dbg_mode;
+    return cb;
+}
+
+void pll_front(const PllCall& c, hipStream_t s)
+{
+    if (c.n == 0) return;
+    // delay-line history for the next call (m samples); this call's kernels read the old one
     {
         LDSP_PROF(s, "k_delay_hist");
-        hipLaunchKernelGGL(k_delay_hist, dim3(1), dim3(64), 0, s, (const float2*)x, (const float2*)hist, (float2*)hist_out,
-                           (long)n, m);
+        hipLaunchKernelGGL(k_delay_hist, dim3(1), dim3(64), 0, s, (const float2*)c.x, (const float2*)c.hist,
+                           (float2*)c.hist_out, (long)c.n, c.m);
+    }
+    LDSP_HIP(hipGetLastError());
+    if (!pll_parallel(c.n)) return;
+    const long nchc = (long)((c.n + kCand - 1) / kCand);
+    {
+        LDSP_PROF(s, "k_pll_cand");
+        static const int warm = std::getenv("LDSP_PLL_WARM") ? std::atoi(std::getenv("LDSP_PLL_WARM")) : kWarm;
+        hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((nchc + 63) / 64)), dim3(64), 0, s, pll_in(c), (long)c.n, c.st,
+                           c.gcur, nchc, cand_buf(c), c.y, warm);
+    }
+    LDSP_HIP(hipGetLastError());
+}
+
+void pll_back(const PllCall& c, hipStream_t s)
+{
+    if (c.n == 0) return;
+    if (!pll_parallel(c.n)) {
+        {
+            LDSP_PROF(s, "k_pll_seq");
+            hipLaunchKernelGGL(k_pll_seq, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
+        }
+        LDSP_HIP(hipGetLastError());
+        return;
+    }
+    const long nblk = (long)((c.n + kBlk - 1) / kBlk);
+    {
+        LDSP_PROF(s, "k_pll_walk");
+        // (a variant deciding the repair direction on the scalar unit, s_cselect over four
+        // readlanes and mask-selected output patches, measured 12 % slower: 5.85 vs 5.21 ms)
+        if (c.alpha_host <= 1.0f / 512.0f)
+            hipLaunchKernelGGL(k_pll_walk<true>, dim3(1), dim3(kWalkThreads), 0, s, pll_in(c), (long)c.n, c.st, nblk,
+                               cand_buf(c), c.y);
+        else
+            hipLaunchKernelGGL(k_pll_walk<false>, dim3(1), dim3(kWalkThreads), 0, s, pll_in(c), (long)c.n, c.st, nblk,
+                               cand_buf(c), c.y);
     }
     LDSP_HIP(hipGetLastError());
 }

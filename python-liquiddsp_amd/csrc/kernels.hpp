@@ -133,17 +133,41 @@ void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y,
 
 // ------------------------------------------------------------------ AmpModem
 struct AmpState {         // device-resident PLL state
-    uint32_t theta, dtheta;
+    uint32_t theta, dtheta;   // true loop state (written by the walker / sequential loop)
     float alpha, beta;
+    uint32_t gth[2], gd[2];   // ping-pong guess of the state at the next call's start (candidate end state)
 };
-// x0 = lowpass(x) (precomputed), x1 = delay_m(x) via hist (m samples); writes
-// m = Re(v1)/mod (carrier) or the final output (Costas) to y.  scratch (of
-// pll_scratch_bytes(n)) enables the chunk-parallel exact path (k_pll.hip).
+// One AmpModem / BroadcastAM PLL call.  x0 = lowpass(x) (precomputed), x1 =
+// delay_m(x) via hist (m samples before x[0]); writes Re(v1)/mod (carrier) or
+// the final output (Costas) to y.  scratch (pll_scratch_bytes(n)) holds the
+// candidate records of the chunk-parallel exact path (k_pll.hip).
+struct PllCall {
+    const void* x0;
+    const void* x;
+    const void* hist;     // m samples before x[0]
+    void* hist_out;       // m samples before the next call's x[0]
+    int m;
+    size_t n;
+    AmpState* st;
+    int gcur;             // candidates start from st->gth/gd[gcur], leave the next guess in [1 - gcur]
+    const float* table;
+    float mod_index;
+    int costas;
+    float alpha_host;
+    float* y;
+    void* scratch;
+};
 size_t pll_scratch_bytes(size_t n);
 size_t pll_stats_offset(size_t n);     // 4 x u64 walker counters inside the scratch (debug)
-void ampmodem_pll(const void* x0, const void* x, const void* hist, void* hist_out, int m, size_t n,
-                  AmpState* st, const float* table, float mod_index, int costas, float alpha_host, float* y, void* scratch,
-                  hipStream_t s);
+// True when the call runs as candidates + walker (else one sequential loop in pll_back).
+bool pll_parallel(size_t n);
+// Front half: the delay-line history for the next call and (parallel calls)
+// the candidate chunks.  Reads only the guess state, never the true state, so
+// it may run while the previous call's pll_back is still walking.
+void pll_front(const PllCall& c, hipStream_t s);
+// Back half: the exact walk over the candidates (or the sequential loop);
+// reads and advances the true state, so it must follow the previous call's back half.
+void pll_back(const PllCall& c, hipStream_t s);
 
 // ------------------------------------------------------------------ debug
 void math_eval(int fn, const float* a, const float* b, float* y, size_t n, hipStream_t s);

@@ -93,6 +93,36 @@ struct DeviceGuard {
     }
 };
 
+// Cross-stream order of one object's device state.  An execute marks the point
+// on its stream where the object's state (and the scratch it reuses) is final;
+// an execute enqueued on a different stream first waits for that point, so
+// calls made on several streams still run in call order per object while
+// different objects (or independent parts of one object) overlap.  Calls on one
+// stream need nothing beyond stream order.
+struct StreamMark {
+    hipEvent_t ev = nullptr;
+    hipStream_t s = nullptr;
+    bool set = false;
+    StreamMark() = default;
+    StreamMark(const StreamMark&) = delete;
+    StreamMark& operator=(const StreamMark&) = delete;
+    ~StreamMark() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    void wait(hipStream_t t) const {
+        if (set && s != t) LDSP_HIP(hipStreamWaitEvent(t, ev, 0));
+    }
+    void mark(hipStream_t t) {
+        if (!ev) LDSP_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        LDSP_HIP(hipEventRecord(ev, t));
+        s = t;
+        set = true;
+    }
+    void sync() const {
+        if (set) LDSP_HIP(hipEventSynchronize(ev));
+    }
+};
+
 int current_device();                       // throws LDSP_EHIP when no GPU is present
 hipStream_t library_stream(int device);     // per-device non-blocking stream for host-memory calls
 

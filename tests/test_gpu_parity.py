@@ -405,6 +405,27 @@ def test_ampmodem_bitwise(ld, ora, rng, carrier):
     assert g.pll_state() == o.pll_state
 
 
+def test_ampmodem_parallel_calls_on_two_streams(ld, ora, rng):
+    # Long calls run as candidates + walker; consecutive calls alternate torch
+    # streams, so call k's candidates overlap call k-1's walk (guess state, two
+    # scratch slots, three history buffers).  Short calls interleave the
+    # sequential loop.  Everything must stay bit-identical to one sequential run.
+    import torch
+    x = _am(rng, 6 * 20_000 + 3000, 48000.0, 300.0, amp=1.0)
+    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
+    o = ora.AmpModem(0.5, "dsb", carrier=True)
+    xd = torch.from_numpy(x).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    cuts = [0, 20_000, 40_000, 41_000, 61_000, 81_000, 101_000, 121_000, len(x)]
+    outs = []
+    for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        with torch.cuda.stream(streams[i % 2]):
+            outs.append(g(xd[a:b]))
+    torch.cuda.synchronize()
+    assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), o(x))
+    assert g.pll_state() == o.pll_state
+
 
 # ------------------------------------------------------------------ helpers either side of the path
 def test_bytes_to_iq_bitwise(ld, ora, rng):
@@ -537,6 +558,22 @@ def test_amradio_exact_bitwise(ld, ora, rng):
     run = _chain(ld, exact=True)
     y = np.concatenate([run(x[i:i + 65536]) for i in range(0, len(x), 65536)])
     assert_bitwise(y, ora.AMRadio()(x))
+
+
+def test_amradio_two_streams_bitwise(ld, ora, rng):
+    # the bench's pipelined form: consecutive chain calls on alternating streams
+    import torch
+    x = _am(rng, 1 << 19, 2e6, 1200.0, amp=0.1)
+    run = _chain(ld, exact=True)
+    xd = torch.from_numpy(x).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    outs = []
+    for i, k in enumerate(range(0, len(x), 1 << 17)):
+        with torch.cuda.stream(streams[i % 2]):
+            outs.append(run(xd[k:k + (1 << 17)]))
+    torch.cuda.synchronize()
+    assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), ora.AMRadio()(x))
 
 
 def test_amradio_fast_close(ld, ora, rng):
