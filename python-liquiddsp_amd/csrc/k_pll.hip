@@ -129,7 +129,7 @@ struct CandBuf {
     uint32_t* ce;         // [nsub][2] candidate state at chunk end
     unsigned long long* stats;   // walker counters: repairs, -, walk ticks, barrier-wait ticks
     long npad;
-    int dbg;              // timing experiments only (LDSP_DEBUG_PLL_MODE): 1 = skip repairs
+    int norep;            // timing experiment (LDSP_DEBUG_PLL=2, counting kernel only): skip every repair
 };
 
 __device__ __forceinline__ const float2* x1_ptr(const PllIn& in, long i)
@@ -175,12 +175,13 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
                 const Kick kc = pll_eval(tab, ic, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
                 if (REC) {
                     const long s = i + j;
+                    const uint32_t jl = (uint32_t)(s & 63);
                     const Kick km = pll_eval(tab, (ic - 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
                     const Kick kp = pll_eval(tab, (ic + 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
-                    cb.rec[2 * s] = make_uint4(theta, (theta + (1u << 21)) & 0x3fffffu, km.k1 - kc.k1, km.k2 - kc.k2);
-                    cb.rec[2 * s + 1] = make_uint4(kp.k1 - kc.k1, kp.k2 - kc.k2, __float_as_uint(km.out),
+                    const uint32_t d1m = km.k1 - kc.k1, d1p = kp.k1 - kc.k1;
+                    cb.rec[2 * s] = make_uint4(theta + (1u << 21), __float_as_uint(kc.out), d1m, km.k2 - kc.k2 - jl * d1m);
+                    cb.rec[2 * s + 1] = make_uint4(d1p, kp.k2 - kc.k2 - jl * d1p, __float_as_uint(km.out),
                                                    __float_as_uint(kp.out));
-                    y[s] = kc.out;
                 }
                 d += kc.k1;
                 theta += kc.k2 + d;
@@ -322,12 +323,14 @@ struct FullCtx {
     const float* table;
     int m, costas;
     float alpha, beta, mod_index;
+    int norep;
 };
 
-// Kick differences and output of the true index (icand + t) at global sample sg.
-__device__ __noinline__ uint4 pll_full(FullCtx fc, uint32_t thc, uint32_t t, long sg)
+// Kick differences and output of the true index (icand + t) at global sample sg;
+// w = candidate theta + 2^21 (record word 0).
+__device__ __noinline__ uint4 pll_full(FullCtx fc, uint32_t w, uint32_t t, long sg)
 {
-    const uint32_t ic = tidx(thc);
+    const uint32_t ic = w >> 22;
     const uint32_t it = (ic + t) & 0x3ffu;
     const long g = sg - fc.m;
     const float2 u0 = fc.x0[sg], u1 = g >= 0 ? fc.x[g] : fc.hist[g + fc.m];
@@ -336,82 +339,7 @@ __device__ __noinline__ uint4 pll_full(FullCtx fc, uint32_t thc, uint32_t t, lon
     return make_uint4(kt.k1 - kc.k1, kt.k2 - kc.k2, __float_as_uint(kt.out), 0u);
 }
 
-__device__ __forceinline__ void load_sub(uint4 (&D)[4][2], const WalkBuf& b, int sub, int lane)
-{
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int i = sub * kCand + q * 64 + lane;
-        D[q][0] = b.rec[2 * i];
-        D[q][1] = b.rec[2 * i + 1];
-    }
-}
-
 __device__ __forceinline__ uint32_t rl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
-
-// lane * m (mod 2^32) for a lane index (< 64): v_mul_i32_i24 when m fits 24
-// signed bits (the usual case), the quarter-rate v_mul_lo_u32 otherwise.
-__device__ __forceinline__ uint32_t lane_mul(uint32_t lane, uint32_t m)
-{
-    const int32_t ms = (int32_t)m;
-    if (ms >= -(1 << 23) && ms < (1 << 23)) return (uint32_t)__mul24((int)lane, ms);
-    return lane * m;
-}
-
-// Walker inner loop, latency-trimmed: per lane-block the offsets v = u + K + l DD
-// live in one VGPR that is updated in place after each repair
-// (v += (dk2 - j dk1) + l dk1), the direction-dependent record words are
-// selected per lane before the readlanes (3 instead of 6), and the rare
-// |di| > 1 case is tested with one scalar bit test.
-template <bool FULL>
-__device__ __forceinline__ void walk_sub2(const uint4 (&D)[4][2], int base0, int cnt, uint32_t& K, uint32_t& DD,
-                                          uint32_t& ldd, float* __restrict__ yb, long sb, int lane,
-                                          const FullCtx& fc, unsigned long long& n_rep)
-{
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int base = base0 + q * 64;
-        int nvalid = 64;
-        if (!FULL) {
-            nvalid = min(64, cnt - base);
-            if (nvalid <= 0) return;
-        }
-        unsigned long long M = (FULL || nvalid == 64) ? ~0ull : ((1ull << nvalid) - 1ull);
-        unsigned long long PM = 0;
-        uint32_t pout = 0;
-        uint32_t v = D[q][0].y + K + lane_mul((uint32_t)lane, DD);
-        while (true) {
-            // index of th + off equals index of th  <=>  u + off < 2^22 (mod 2^32)
-            const unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
-            if (mask == 0) break;
-            const int j = __builtin_ctzll(mask);
-            const bool upl = v - 0x400000u < 0x400000u;                  // di = +1
-            const bool dnl = v >= 0xffc00000u;                          // di = -1
-            const unsigned long long bigm = __builtin_amdgcn_ballot_w64(!upl && !dnl);
-            const uint32_t sdk1 = upl ? D[q][1].x : D[q][0].z;
-            const uint32_t sdk2 = upl ? D[q][1].y : D[q][0].w;
-            const uint32_t sout = upl ? D[q][1].w : D[q][1].z;
-            uint32_t dk1 = rl(sdk1, j), dk2 = rl(sdk2, j), ob = rl(sout, j);
-            if ((bigm >> j) & 1ull) {                                   // rare: |di| > 1
-                const uint4 f = pll_full(fc, rl(D[q][0].x, j), rl(v, j) >> 22, sb + base + j);
-                dk1 = __builtin_amdgcn_readfirstlane(f.x);
-                dk2 = __builtin_amdgcn_readfirstlane(f.y);
-                ob = __builtin_amdgcn_readfirstlane(f.z);
-            }
-            n_rep++;
-            pout = lane == j ? ob : pout;
-            PM |= 1ull << j;
-            const uint32_t c = dk2 - (uint32_t)j * dk1;
-            K += c;
-            DD += dk1;
-            v += c + lane_mul((uint32_t)lane, dk1);
-            M &= (~0ull << j) << 1;
-        }
-        if (PM != 0 && ((PM >> lane) & 1ull)) yb[base + lane] = __uint_as_float(pout);
-        K += (uint32_t)nvalid * DD;
-        if (!FULL && nvalid < 64) break;
-    }
-    ldd = lane_mul((uint32_t)lane, DD);
-}
 
 // v + lane * dk1.  F24: every kick difference fits 24 signed bits (host check:
 // |k1| <= alpha 2^31, so |dk1| < 2^23 when alpha <= 2^-9), one v_mad_i32_i24.
@@ -426,67 +354,140 @@ __device__ __forceinline__ uint32_t mad_lane(uint32_t lane, uint32_t dk1, uint32
     return v + lane * dk1;
 }
 
-// Repair loop with the fewest dependent instructions found: mismatch / +1 /
-// |di| > 1 classes from three compares, direction-selected record words read
-// back with three readlanes, the patched output written into lane j with
-// v_writelane, the per-lane offset advanced with one 24-bit multiply-add.
-template <bool FULL, bool F24>
-__device__ __forceinline__ void walk_sub3(const uint4 (&D)[4][2], int base0, int cnt, uint32_t& K, uint32_t& DD,
-                                          uint32_t& ldd, float* __restrict__ yb, long sb, int lane,
-                                          const FullCtx& fc, unsigned long long n_rep, unsigned& nrep)
+// pout = lane is set in `bit` ? so : pout  (one v_cndmask_b32 with an SGPR lane mask)
+__device__ __forceinline__ uint32_t sel_lane(uint32_t pout, uint32_t so, unsigned long long bit)
+{
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(pout), "v"(so), "s"(bit));
+    return r;
+}
+
+// Walker state per lane-block of 64 samples.  Record words (k_pll_cand):
+//   R0 = (w = th + 2^21, candidate output, dk1(i-1), dk2'(i-1))
+//   R1 = (dk1(i+1), dk2'(i+1), output(i-1), output(i+1))
+// with dk2' = dk2 - (s mod 64) dk1, so that a repair at lane j adds
+// dk2' + lane dk1 to the offset of every lane (only lanes > j matter).
+// v = u + offset per lane, u = w mod 2^22 the candidate's position in its
+// table cell: the true index equals the candidate's iff v < 2^22; it is one
+// cell up iff 2^22 <= v < 2^23, one down iff v >= 2^32 - 2^22, else |di| > 1.
+
+// Any-distance repair loop over the lanes in M, in order (block tails, the
+// rare |di| > 1 samples): the direction is decided on the scalar unit and
+// |di| > 1 re-evaluates the loop step (pll_full).  By value in and out: a
+// reference would put the caller's registers on the stack.
+struct WalkRegs {
+    uint32_t v, pout, DD, nrep;
+};
+template <bool F24>
+__device__ __noinline__ WalkRegs walk_generic(uint4 R0, uint4 R1, WalkRegs r, unsigned long long M, long sg0, int lane,
+                                              FullCtx fc)
+{
+    uint32_t DD = __builtin_amdgcn_readfirstlane(r.DD);
+    unsigned long long mask = __builtin_amdgcn_ballot_w64(r.v > 0x3fffffu) & M;
+    while (mask != 0) {
+        const int j = __builtin_ctzll(mask);
+        const uint32_t vj = rl(r.v, j);
+        uint32_t dk1, dk2p, ob;
+        if (vj - 0x400000u < 0x400000u) {
+            dk1 = rl(R1.x, j);
+            dk2p = rl(R1.y, j);
+            ob = rl(R1.w, j);
+        } else if (vj >= 0xffc00000u) {
+            dk1 = rl(R0.z, j);
+            dk2p = rl(R0.w, j);
+            ob = rl(R1.z, j);
+        } else {
+            const uint4 f = pll_full(fc, rl(R0.x, j), vj >> 22, sg0 + j);
+            dk1 = __builtin_amdgcn_readfirstlane(f.x);
+            dk2p = __builtin_amdgcn_readfirstlane(f.y) - (uint32_t)j * dk1;
+            ob = __builtin_amdgcn_readfirstlane(f.z);
+        }
+        r.pout = lane == j ? ob : r.pout;
+        r.v = mad_lane<F24>((uint32_t)lane, dk1, r.v) + dk2p;
+        DD += dk1;
+        r.nrep++;
+        M &= (~0ull << j) << 1;
+        mask = __builtin_amdgcn_ballot_w64(r.v > 0x3fffffu) & M;
+    }
+    r.DD = DD;
+    return r;
+}
+
+// Full lane-block fast path, assuming every repaired lane is one cell away:
+// per repair one ff1, three direction selects, two readlanes, two lane selects
+// (the output, and v at the repair for the check below), a 24-bit
+// multiply-add and an add for the offsets, one ballot.  Afterwards one ballot
+// over the repaired lanes checks that assumption; if any was |di| > 1 (rare:
+// loop unlocked) the whole block is redone by walk_generic from its start.
+template <bool F24, bool STATS>
+__device__ __forceinline__ void walk_block(const uint4& R0, const uint4& R1, uint32_t& v, uint32_t& DD, float* yb,
+                                           long sg0, int lane, const FullCtx& fc, unsigned& nrep)
+{
+    const uint32_t v_in = v, dd_in = DD;
+    uint32_t pout = R0.y, vrep = 0;
+    unsigned long long PM = 0;
+    unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu);
+    if (STATS && fc.norep) mask = 0;
+    unsigned cnt = 0;
+    while (mask != 0) {
+        const int j = __builtin_ctzll(mask);
+        const bool upl = v < 0x800000u;                               // one cell up (else down)
+        const uint32_t s1 = upl ? R1.x : R0.z;
+        const uint32_t s2 = upl ? R1.y : R0.w;
+        const uint32_t so = upl ? R1.w : R1.z;
+        const uint32_t dk1 = rl(s1, j), dk2p = rl(s2, j);
+        const unsigned long long bit = 1ull << j;
+        pout = sel_lane(pout, so, bit);
+        vrep = sel_lane(vrep, v, bit);
+        PM |= bit;
+        v = mad_lane<F24>((uint32_t)lane, dk1, v) + dk2p;
+        DD += dk1;
+        if (STATS) cnt++;
+        mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & ((~0ull << j) << 1);
+    }
+    if (__builtin_expect((__builtin_amdgcn_ballot_w64(vrep + 0x400000u > 0xbfffffu) & PM) != 0, 0)) {
+        WalkRegs r{v_in, R0.y, dd_in, nrep};
+        r = walk_generic<F24>(R0, R1, r, ~0ull, sg0, lane, fc);
+        v = r.v;
+        pout = r.pout;
+        DD = __builtin_amdgcn_readfirstlane(r.DD);
+        if (STATS) nrep = __builtin_amdgcn_readfirstlane(r.nrep);
+    } else if (STATS) {
+        nrep += cnt;
+    }
+    yb[lane] = __uint_as_float(pout);
+}
+
+__device__ __forceinline__ void load_sub(uint4 (&D)[4][2], const WalkBuf& b, int sub, int lane)
 {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const int base = base0 + q * 64;
-        int nvalid = 64;
-        if (!FULL) {
-            nvalid = min(64, cnt - base);
-            if (nvalid <= 0) return;
-        }
-        unsigned long long M = (FULL || nvalid == 64) ? ~0ull : ((1ull << nvalid) - 1ull);
-        unsigned long long PM = 0;
-        uint32_t pout = 0;
-        uint32_t v = D[q][0].y + K + ldd;                // ldd = lane * DD (mod 2^32)
-        unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
-        if (n_rep == 1) mask = 0;      // timing experiment (LDSP_DEBUG_PLL_MODE=1): skip repairs
-        while (mask != 0) {
-            const int j = __builtin_ctzll(mask);
-            const unsigned long long bigm = __builtin_amdgcn_ballot_w64(v + 0x400000u > 0xbfffffu);
-            const bool upl = v - 0x400000u < 0x400000u;                  // di = +1 (else -1)
-            const uint32_t sdk1 = upl ? D[q][1].x : D[q][0].z;
-            const uint32_t sdk2 = upl ? D[q][1].y : D[q][0].w;
-            const uint32_t sout = upl ? D[q][1].w : D[q][1].z;
-            uint32_t dk1 = rl(sdk1, j), dk2 = rl(sdk2, j), ob = rl(sout, j);
-            if (__builtin_expect((bigm >> j) & 1ull, 0)) {              // rare: |di| > 1
-                const uint4 f = pll_full(fc, rl(D[q][0].x, j), rl(v, j) >> 22, sb + base + j);
-                dk1 = __builtin_amdgcn_readfirstlane(f.x);
-                dk2 = __builtin_amdgcn_readfirstlane(f.y);
-                ob = __builtin_amdgcn_readfirstlane(f.z);
-            }
-            {
-                unsigned keep;    // M0 is compiler-reserved: save and restore it in the same statement
-                asm volatile("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
-                             : "+v"(pout), "=&s"(keep)
-                             : "s"(ob), "s"(j));
-            }
-            PM |= 1ull << j;
-            K += dk2 - (uint32_t)j * dk1;
-            DD += dk1;
-            nrep++;
-            ldd = mad_lane<F24>((uint32_t)lane, dk1, ldd);
-            v = D[q][0].y + K + ldd;
-            M &= (~0ull << j) << 1;
-            mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
-        }
-        if ((PM >> lane) & 1ull) yb[base + lane] = __uint_as_float(pout);
-        K += (uint32_t)nvalid * DD;
-        if (!FULL && nvalid < 64) break;
+        const int i = sub * kCand + q * 64 + lane;
+        D[q][0] = b.rec[2 * i];
+        D[q][1] = b.rec[2 * i + 1];
     }
 }
 
-// Wave 0 walks block c; waves 1-7 store block c+1 (fetched into registers
-// during the previous block) into the other LDS buffer and fetch block c+2.
-template <bool F24>
+// The four lane-blocks of one candidate chunk.
+template <bool F24, bool STATS>
+__device__ __forceinline__ void walk_sub(const uint4 (&D)[4][2], int sub, uint32_t& off, uint32_t& DD, float* yb, long s0,
+                                         int lane, const FullCtx& fc, unsigned& nrep)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int base = sub * kCand + q * 64;
+        const uint32_t u = D[q][0].x & 0x3fffffu;
+        uint32_t v = u + off;
+        walk_block<F24, STATS>(D[q][0], D[q][1], v, DD, yb + base, s0 + base, lane, fc, nrep);
+        off = v - u + 64u * DD;
+    }
+}
+
+// Wave 0 walks block c; waves 1-7 DMA the records of block c + 3 into the LDS
+// ring meanwhile.  Per lane the walker carries off = the exact offset of the
+// true trajectory from the current candidate chunk at its sample (affine in
+// the lane: K + lane DD), DD = the frequency offset (wave-uniform).
+template <bool F24, bool STATS>
 __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, long nblk, CandBuf cb,
                                                            float* __restrict__ y)
 {
@@ -515,11 +516,12 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     fc.alpha = st->alpha;
     fc.beta = st->beta;
     fc.mod_index = in.mod_index;
+    fc.norep = STATS ? cb.norep : 0;
     uint32_t th_t = st->theta, d_t = st->dtheta;      // true state at the current block start
-    unsigned long long n_rep = (unsigned long long)__builtin_amdgcn_readfirstlane(cb.dbg), cyc_walk = 0, cyc_wait = 0;
+    unsigned long long cyc_walk = 0, cyc_wait = 0;
     unsigned nrep = 0;
     for (long c = 0; c < nblk; c++) {
-        const unsigned long long t0 = wall_clock64();
+        const unsigned long long t0 = STATS ? wall_clock64() : 0;
         if (wave != 0) {
             // slot (c + 3) & 3 held block c - 1, released by the previous barrier
             if (c + 3 < nblk) walk_dma(buf[(c + 3) & 3], cb, c + 3, lw, lane);
@@ -532,13 +534,10 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             const long s0 = c * kBlk;
             const int cnt = (int)min((long)kBlk, n - s0);
             float* yb = y + s0;
-            // Offset of the true trajectory from the candidate (exact, mod 2^32):
-            // at local sample base + l of the current lane-block, dtheta = K + l*DD.
             // candidate chunk start / end states of the block (cs[0..7], ce[0..7]) in one LDS read
             const uint32_t csce = lane < 2 * kSub ? b.cs[lane] : (lane < 4 * kSub ? b.ce[lane - 2 * kSub] : 0u);
-            uint32_t K = th_t - rl(csce, 0);
             uint32_t DD = d_t - rl(csce, 1);
-            uint32_t ldd = (uint32_t)lane * DD;
+            uint32_t off = th_t - rl(csce, 0) + (uint32_t)lane * DD;
             uint4 D0[4][2], D1[4][2];
             load_sub(D0, b, 0, lane);
             int last = 0;
@@ -546,53 +545,72 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
 #pragma unroll
                 for (int sub = 0; sub < kSub; sub++) {
                     if (sub > 0) {                                  // next candidate chunk: rebase the offset
-                        K = rl(csce, 2 * kSub + 2 * sub - 2) + K - rl(csce, 2 * sub);
-                        DD = rl(csce, 2 * kSub + 2 * sub - 1) + DD - rl(csce, 2 * sub + 1);
-                        ldd = (uint32_t)lane * DD;
+                        const uint32_t dth = rl(csce, 2 * kSub + 2 * sub - 2) - rl(csce, 2 * sub);
+                        const uint32_t dd = rl(csce, 2 * kSub + 2 * sub - 1) - rl(csce, 2 * sub + 1);
+                        off += dth + (uint32_t)lane * dd;
+                        DD += dd;
                     }
                     if (sub & 1) {
                         if (sub + 1 < kSub) load_sub(D0, b, sub + 1, lane);
-                        walk_sub3<true, F24>(D1, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, nrep);
+                        walk_sub<F24, STATS>(D1, sub, off, DD, yb, s0, lane, fc, nrep);
                     } else {
                         if (sub + 1 < kSub) load_sub(D1, b, sub + 1, lane);
-                        walk_sub3<true, F24>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, nrep);
+                        walk_sub<F24, STATS>(D0, sub, off, DD, yb, s0, lane, fc, nrep);
                     }
                 }
                 last = kSub - 1;
             } else {
                 for (int sub = 0; sub * kCand < cnt; sub++) {
                     if (sub > 0) {
-                        K = rl(csce, 2 * kSub + 2 * sub - 2) + K - rl(csce, 2 * sub);
-                        DD = rl(csce, 2 * kSub + 2 * sub - 1) + DD - rl(csce, 2 * sub + 1);
-                        ldd = (uint32_t)lane * DD;
+                        const uint32_t dth = rl(csce, 2 * kSub + 2 * sub - 2) - rl(csce, 2 * sub);
+                        const uint32_t dd = rl(csce, 2 * kSub + 2 * sub - 1) - rl(csce, 2 * sub + 1);
+                        off += dth + (uint32_t)lane * dd;
+                        DD += dd;
                     }
                     load_sub(D0, b, sub, lane);
-                    walk_sub3<false, F24>(D0, sub * kCand, cnt, K, DD, ldd, yb, s0, lane, fc, n_rep, nrep);
+                    for (int q = 0; q < 4; q++) {
+                        const int base = sub * kCand + q * 64;
+                        const int nvalid = min(64, cnt - base);
+                        if (nvalid <= 0) break;
+                        const uint32_t u = D0[q][0].x & 0x3fffffu;
+                        uint32_t v = u + off;
+                        const unsigned long long M = nvalid == 64 ? ~0ull : ((1ull << nvalid) - 1ull);
+                        WalkRegs r{v, D0[q][0].y, DD, nrep};
+                        r = walk_generic<F24>(D0[q][0], D0[q][1], r, M, s0 + base, lane, fc);
+                        v = r.v;
+                        DD = __builtin_amdgcn_readfirstlane(r.DD);
+                        nrep = __builtin_amdgcn_readfirstlane(r.nrep);
+                        if (lane < nvalid) yb[base + lane] = __uint_as_float(r.pout);
+                        off = v - u + (uint32_t)nvalid * DD;
+                    }
                     last = sub;
                 }
             }
-            // true state at the block end = candidate end + offset at cnt
-            th_t = b.ce[2 * last] + K;
+            // true state at the block end = candidate end + offset there (lane 0 of off)
+            th_t = b.ce[2 * last] + __builtin_amdgcn_readfirstlane(off);
             d_t = b.ce[2 * last + 1] + DD;
-            (void)csce;
         }
         // LDS-only barrier: __syncthreads() would also drain the loaders' global fetch of
         // block c + 2 (vmcnt(0)), putting an HBM round trip into every block
-        const unsigned long long t1 = wall_clock64();
+        const unsigned long long t1 = STATS ? wall_clock64() : 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        const unsigned long long t2 = wall_clock64();
-        cyc_walk += t1 - t0;
-        cyc_wait += t2 - t1;
+        if (STATS) {
+            const unsigned long long t2 = wall_clock64();
+            cyc_walk += t1 - t0;
+            cyc_wait += t2 - t1;
+        }
     }
     if (tid == 0) {
         st->theta = th_t;
         st->dtheta = d_t;
-        cb.stats[0] = nrep;
-        cb.stats[1] = 0;
-        cb.stats[2] = cyc_walk;
-        cb.stats[3] = cyc_wait;
+        if (STATS) {
+            cb.stats[0] = nrep;
+            cb.stats[1] = 0;
+            cb.stats[2] = cyc_walk;
+            cb.stats[3] = cyc_wait;
+        }
     }
 }
 
@@ -645,8 +663,8 @@ static CandBuf cand_buf(const PllCall& c)
     cb.cs = (uint32_t*)(p + (size_t)cb.npad * 32);
     cb.ce = cb.cs + 2 * nblk * kSub;
     cb.stats = (unsigned long long*)(p + pll_stats_offset(c.n));
-    static const int dbg_mode = std::getenv("LDSP_DEBUG_PLL_MODE") ? std::atoi(std::getenv("LDSP_DEBUG_PLL_MODE")) : 0;
-    cb.dbg = dbg_mode;
+    static const int dbg = std::getenv("LDSP_DEBUG_PLL") ? std::atoi(std::getenv("LDSP_DEBUG_PLL")) : 0;
+    cb.norep = dbg == 2;
     return cb;
 }
 
@@ -685,14 +703,17 @@ void pll_back(const PllCall& c, hipStream_t s)
     const long nblk = (long)((c.n + kBlk - 1) / kBlk);
     {
         LDSP_PROF(s, "k_pll_walk");
-        // (a variant deciding the repair direction on the scalar unit, s_cselect over four
-        // readlanes and mask-selected output patches, measured 12 % slower: 5.85 vs 5.21 ms)
-        if (c.alpha_host <= 1.0f / 512.0f)
-            hipLaunchKernelGGL(k_pll_walk<true>, dim3(1), dim3(kWalkThreads), 0, s, pll_in(c), (long)c.n, c.st, nblk,
-                               cand_buf(c), c.y);
-        else
-            hipLaunchKernelGGL(k_pll_walk<false>, dim3(1), dim3(kWalkThreads), 0, s, pll_in(c), (long)c.n, c.st, nblk,
-                               cand_buf(c), c.y);
+        static const bool stats = std::getenv("LDSP_DEBUG_PLL") != nullptr;
+        const dim3 g(1), blk(kWalkThreads);
+        const PllIn in = pll_in(c);
+        const CandBuf cb = cand_buf(c);
+        if (c.alpha_host <= 1.0f / 512.0f) {
+            if (stats) hipLaunchKernelGGL((k_pll_walk<true, true>), g, blk, 0, s, in, (long)c.n, c.st, nblk, cb, c.y);
+            else hipLaunchKernelGGL((k_pll_walk<true, false>), g, blk, 0, s, in, (long)c.n, c.st, nblk, cb, c.y);
+        } else {
+            if (stats) hipLaunchKernelGGL((k_pll_walk<false, true>), g, blk, 0, s, in, (long)c.n, c.st, nblk, cb, c.y);
+            else hipLaunchKernelGGL((k_pll_walk<false, false>), g, blk, 0, s, in, (long)c.n, c.st, nblk, cb, c.y);
+        }
     }
     LDSP_HIP(hipGetLastError());
 }
