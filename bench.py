@@ -176,10 +176,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-components", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the steps rotate over (1 = every step on torch's current stream). "
                          "Each object orders its own calls across streams (libldsp StreamMark), so step k+1's "
                          "IIR/resampler/AGC/candidate kernels overlap step k's serial PLL walk")
+    ap.add_argument("--no-kprof", action="store_true",
+                    help="no per-kernel HIP events inside the timed steps (kernel times then come from a separate "
+                         "profiled pass)")
     ap.add_argument("--scatter", action="store_true",
                     help="rank 0 holds all channels: every step scatters the IQ blocks and gathers the PCM "
                          "(SURVEY 8e) instead of each rank reading a resident channel")
@@ -213,7 +216,10 @@ def main():
     streams = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(nstreams - 1)]
     barrier = tdist.barrier if dist else (lambda: None)
 
+    host = {"t": 0.0}
+
     def step(k, prof=True, rot=nstreams):
+        h0 = time.perf_counter()
         if k == 0 and prof:
             L._profile_reset()                 # per-kernel HIP events over exactly the timed steps
             L._profile_enable(True)
@@ -222,8 +228,14 @@ def main():
             out["y"] = radio(xin, events[k] if (k is not None and prof) else None)
         if args.scatter and dist:
             gather_pcm(out["y"])
+        if k is not None:
+            host["t"] += time.perf_counter() - h0
 
-    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, barrier)
+    kp = not args.no_kprof
+    elapsed = timed_steps(lambda k: step(k, prof=kp), args.steps, args.warmup, torch.cuda.synchronize, barrier)
+    host_ms = host["t"] / args.steps * 1e3
+    if not kp:          # kernel / stage times from a separate profiled pass over the same steps
+        timed_steps(step, args.steps, 0, torch.cuda.synchronize, barrier)
     L._profile_enable(False)
     kprof = L._profile_report()
     # the same chain with every step on one stream (no overlap between steps), for reference
@@ -282,6 +294,8 @@ def main():
                      "note": "alg bytes = 12 B per PCM sample (AmpModem in + out); the PLL recurrence is "
                              "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else ""},
         "streams": nstreams,
+        "host_ms_per_step": round(host_ms, 4),
+        "kernel_events_in_timed_steps": kp,
         "single_stream_ms_per_step": round(single / single_steps * 1e3, 4),
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "kernels": kernels,

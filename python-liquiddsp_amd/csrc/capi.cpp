@@ -702,16 +702,29 @@ std::mutex g_mu;
 struct Pending {
     const char* name;
     hipEvent_t a, b;
+    hipStream_t s;
 };
 std::vector<Pending> g_pending;
 std::vector<std::pair<std::string, std::pair<long, double>>> g_done;   // name -> (calls, total ms)
 
+// LDSP_PROF_TIMELINE=<file>: also append every profiled launch as
+// "name stream start_ms end_ms" relative to the first launch since the last
+// reset (overlap and gaps between streams; diagnostics only).
+hipEvent_t g_t0 = nullptr;
 void drain_locked()
 {
+    static const char* tl_path = std::getenv("LDSP_PROF_TIMELINE");
+    FILE* tl = tl_path ? std::fopen(tl_path, "a") : nullptr;
     for (auto& r : g_pending) {
         float ms = 0.0f;
         if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&ms, r.a, r.b);
-        (void)hipEventDestroy(r.a);
+        if (tl) {
+            if (!g_t0) g_t0 = r.a;
+            float t0 = 0.0f;
+            (void)hipEventElapsedTime(&t0, g_t0, r.a);
+            std::fprintf(tl, "%s %p %.4f %.4f\n", r.name, (void*)r.s, t0, t0 + ms);
+        }
+        if (r.a != g_t0) (void)hipEventDestroy(r.a);     // the origin lives until the next reset
         (void)hipEventDestroy(r.b);
         auto it = std::find_if(g_done.begin(), g_done.end(), [&](const auto& e) { return e.first == r.name; });
         if (it == g_done.end()) g_done.push_back({r.name, {1, (double)ms}});
@@ -721,6 +734,7 @@ void drain_locked()
         }
     }
     g_pending.clear();
+    if (tl) std::fclose(tl);
 }
 } // namespace
 
@@ -741,7 +755,7 @@ Scope::~Scope()
         return;
     }
     std::lock_guard<std::mutex> lk(g_mu);
-    g_pending.push_back({name, a, b});
+    g_pending.push_back({name, a, b, s});
     if (g_pending.size() > 4096) drain_locked();
 }
 } // namespace prof
@@ -761,6 +775,8 @@ int ldsp_profile_reset(void)
         std::lock_guard<std::mutex> lk{ldsp::prof::g_mu};
         ldsp::prof::drain_locked();
         ldsp::prof::g_done.clear();
+        if (ldsp::prof::g_t0) (void)hipEventDestroy(ldsp::prof::g_t0);
+        ldsp::prof::g_t0 = nullptr;
     });
 }
 

@@ -478,6 +478,11 @@ __device__ __forceinline__ void walk_sub(const uint4 (&D)[4][2], int sub, uint32
         const int base = sub * kCand + q * 64;
         const uint32_t u = D[q][0].x & 0x3fffffu;
         uint32_t v = u + off;
+        if (STATS && fc.norep >= 2) {
+            if (fc.norep == 2) yb[base + lane] = __uint_as_float(D[q][0].y);
+            off = v - u + 64u * DD;
+            continue;
+        }
         walk_block<F24, STATS>(D[q][0], D[q][1], v, DD, yb + base, s0 + base, lane, fc, nrep);
         off = v - u + 64u * DD;
     }
@@ -664,7 +669,7 @@ static CandBuf cand_buf(const PllCall& c)
     cb.ce = cb.cs + 2 * nblk * kSub;
     cb.stats = (unsigned long long*)(p + pll_stats_offset(c.n));
     static const int dbg = std::getenv("LDSP_DEBUG_PLL") ? std::atoi(std::getenv("LDSP_DEBUG_PLL")) : 0;
-    cb.norep = dbg == 2;
+    cb.norep = dbg >= 2 ? dbg - 1 : 0;     // 2: skip repairs; 3: skip the lane-block walk; 4: 3 without stores
     return cb;
 }
 
