@@ -1662,12 +1662,12 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     k::pll_back(c, e.stream);
     if (!par) q->front.mark(e.stream);
     if (par && std::getenv("LDSP_DEBUG_PLL")) {
-        unsigned long long stt[4];
+        unsigned long long stt[5];
         LDSP_HIP(hipMemcpyAsync(stt, (char*)c.scratch + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
                                 e.stream));
         LDSP_HIP(hipStreamSynchronize(e.stream));
-        std::fprintf(stderr, "[ldsp pll] n=%zu repairs=%llu unused=%llu walk_clk=%llu wait_clk=%llu\n", n, stt[0],
-                     stt[1], stt[2], stt[3]);
+        std::fprintf(stderr, "[ldsp pll] n=%zu entries=%llu repairs=%llu fallback_lane_blocks=%llu walk_clk=%llu "
+                     "wait_clk=%llu\n", n, stt[4], stt[0], stt[1], stt[2], stt[3]);
     }
     return mbuf;
 }
