@@ -80,15 +80,16 @@ class AMRadio:
 
 def timed_steps(step, steps, warmup, sync, barrier):
     """W untimed warmup steps, then exactly K steps bracketed by a barrier and a
-    device synchronize on both sides; returns this rank's wall time (s)."""
-    for _ in range(warmup):
-        step(None)
+    device synchronize on both sides; returns this rank's wall time (s).
+    step(k, w) gets the timed index k (None while warming up) and the warmup index w."""
+    for w in range(warmup):
+        step(None, w)
     sync()
     barrier()
     sync()
     t0 = time.perf_counter()
     for k in range(steps):
-        step(k)
+        step(k, None)
     sync()
     barrier()
     return time.perf_counter() - t0
@@ -170,7 +171,7 @@ def cpu_baseline(n_iq, seconds=10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -216,30 +217,36 @@ def main():
     streams = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(nstreams - 1)]
     barrier = tdist.barrier if dist else (lambda: None)
 
-    host = {"t": 0.0}
+    host = {"t": 0.0, "max": 0.0}
 
-    def step(k, prof=True, rot=nstreams):
+    def step(k, w=None, prof=True, rot=nstreams):
+        # warmup steps rotate over the streams too: the first use of a stream makes torch's
+        # caching allocator map fresh 512 MB blocks for it, which must not land in the timed steps
         h0 = time.perf_counter()
         if k == 0 and prof:
             L._profile_reset()                 # per-kernel HIP events over exactly the timed steps
             L._profile_enable(True)
         xin = scatter_channels(x_all, args.n, device) if (args.scatter and dist) else x
-        with torch.cuda.stream(streams[(k or 0) % rot]):
+        with torch.cuda.stream(streams[(k if k is not None else (w or 0)) % rot]):
             out["y"] = radio(xin, events[k] if (k is not None and prof) else None)
         if args.scatter and dist:
             gather_pcm(out["y"])
         if k is not None:
-            host["t"] += time.perf_counter() - h0
+            dt = time.perf_counter() - h0
+            host["t"] += dt
+            host["max"] = max(host["max"], dt)
 
     kp = not args.no_kprof
-    elapsed = timed_steps(lambda k: step(k, prof=kp), args.steps, args.warmup, torch.cuda.synchronize, barrier)
+    elapsed = timed_steps(lambda k, w: step(k, w, prof=kp), args.steps, args.warmup, torch.cuda.synchronize, barrier)
     host_ms = host["t"] / args.steps * 1e3
+    host_max_ms = host["max"] * 1e3
     if not kp:          # kernel / stage times from a separate profiled pass over the same steps
         timed_steps(step, args.steps, 0, torch.cuda.synchronize, barrier)
     L._profile_enable(False)
     kprof = L._profile_report()
     # the same chain with every step on one stream (no overlap between steps), for reference
-    single = timed_steps(lambda k: step(k, prof=False, rot=1), min(args.steps, 5), 1, torch.cuda.synchronize, barrier)
+    single = timed_steps(lambda k, w: step(k, w, prof=False, rot=1), min(args.steps, 5), 1, torch.cuda.synchronize,
+                         barrier)
     single_steps = min(args.steps, 5)
     if dist:
         elapsed = reduce_max(elapsed, device)
@@ -295,6 +302,7 @@ def main():
                              "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else ""},
         "streams": nstreams,
         "host_ms_per_step": round(host_ms, 4),
+        "host_ms_max_step": round(host_max_ms, 4),
         "kernel_events_in_timed_steps": kp,
         "single_stream_ms_per_step": round(single / single_steps * 1e3, 4),
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},

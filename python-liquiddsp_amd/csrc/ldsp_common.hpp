@@ -2,6 +2,8 @@
 // HIP checks, grow-only device buffers, stream selection.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 #include <stdexcept>
@@ -69,12 +71,18 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
     }
+    // Grows only: geometric (x1.25) and rounded up to 64 KiB, because every
+    // regrowth frees the old buffer and hipFree waits for the whole device --
+    // a block size that varies by one sample between calls (resampler output)
+    // must not stall the host in steady state.
     void* ensure(size_t bytes, int dev) {
         if (bytes <= cap && p) return p;
         release();
         device = dev;
-        LDSP_HIP(hipMalloc(&p, bytes ? bytes : 16));
-        cap = bytes;
+        size_t want = std::max(bytes, cap + cap / 4);
+        want = (std::max<size_t>(want, 16) + 65535) & ~(size_t)65535;
+        LDSP_HIP(hipMalloc(&p, want));
+        cap = want;
         return p;
     }
     template <typename T> T* as() const { return static_cast<T*>(p); }

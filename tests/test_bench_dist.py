@@ -38,7 +38,7 @@ def _rank_main(rank, world, port, outdir):
     radio = O.AMRadio()
     outs = []
 
-    def step(k):
+    def step(k, w=None):
         outs.append(np.concatenate([radio(x[i:i + 65536]) for i in range(0, n, 65536)]))
 
     mine = bench.timed_steps(step, 2, 1, lambda: None, dist.barrier)
