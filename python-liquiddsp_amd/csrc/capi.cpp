@@ -507,11 +507,19 @@ struct AgcObj {
     k::AgcState h{};                  // host mirror
     float bandwidth = 0.01f;
     int device = -1;
-    DevBuf dst, scratch, status;
+    DevBuf dst, status;
+    // Per-call scratch in two slots (call parity) and the input history the
+    // speculative warm-ups read (the last hist_len samples before the call,
+    // ping-ponged: call k reads hist[k & 1] and writes hist[(k + 1) & 1]).
+    DevBuf scr[2], hist[2];
+    long hist_len = 0, hist_valid = 0;
+    uint64_t ncall = 0;
     bool dev_newer = false;           // device state advanced past the mirror
     bool upload_pending = true;
     hipStream_t last = nullptr;
-    StreamMark ord;                   // cross-stream call order (ldsp_common.hpp)
+    // Cross-stream order (ldsp_common.hpp): ord = back halves (the true
+    // state), front = front halves (history), slot[s] = scratch slot s free.
+    StreamMark ord, front, slot[2];
     Staging stg;
     void init()
     {
@@ -1495,6 +1503,10 @@ int ldsp_agc_set_mode(ldsp_agc_t q, int mode)
     });
 }
 
+// Two halves per call (k_agc.hip): the front runs the speculative chunks --
+// from the input history alone once it holds hist_len samples, so call k + 1's
+// front overlaps call k's back half on another stream -- and the back half
+// checks chunk 0 against the true state, repairs and verifies, and advances it.
 int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* status, int mem, void* stream)
 {
     return guard([&] {
@@ -1503,8 +1515,11 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         q->ensure_device();
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
-        q->ord.wait(e.stream);
+        const int sl = (int)(q->ncall & 1);
+        q->slot[sl].wait(e.stream);
+        q->front.wait(e.stream);
         if (q->upload_pending) {
+            q->ord.wait(e.stream);
             LDSP_HIP(hipStreamSynchronize(e.stream));
             LDSP_HIP(hipMemcpy(q->dst.p, &q->h, sizeof(q->h), hipMemcpyHostToDevice));
             q->upload_pending = false;
@@ -1512,36 +1527,55 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         const void* dx = q->stg.dev_in(e, x, n * 8);
         void* dy = q->stg.dev_out(e, y, n * 8);
         uint8_t* dstat = status ? (uint8_t*)q->status.ensure(std::max<size_t>(n, 1), q->device) : nullptr;
+        // exact warm-up W = 20/bandwidth after an approximate one of Wa = 40/bandwidth
+        // (k_agc.hip); measured on the AM chain at bandwidth 0.01 the exact loop then
+        // coalesces within ~110 samples on average, 2834 at worst.
+        const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
+        static const float wmul = std::getenv("LDSP_AGC_WMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WMUL")) : 20.0f;
+        static const float wamul = std::getenv("LDSP_AGC_WAMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WAMUL")) : 40.0f;
+        static const int rounds = std::getenv("LDSP_AGC_ROUNDS") ? std::atoi(std::getenv("LDSP_AGC_ROUNDS")) : 3;
+        static const bool nospec = std::getenv("LDSP_AGC_NOSPEC") != nullptr;   // A/B: every call from the true state
+        const int W = (int)std::min(1 << 18, std::max(256, (int)(wmul / a)));
+        const int Wa = (int)std::min(1 << 20, std::max(1024, (int)(wamul / a)));
+        const long hl = (long)W + Wa + k::kAgcPow;
+        if (hl != q->hist_len) {             // bandwidth changed: history restarts
+            q->hist_len = hl;
+            q->hist_valid = 0;
+            q->hist[0].ensure((size_t)hl * 8, q->device);
+            q->hist[1].ensure((size_t)hl * 8, q->device);
+        }
+        const bool spec = !nospec && q->hist_valid >= hl;
+        const bool par = n >= (size_t)4 * (W + Wa);
+        k::SpecPlan p;
+        if (n > 0 && par) {
+            p.W = W;
+            p.Wa = Wa;
+            p.rounds = std::max(0, std::min(rounds, 6));
+            p.C = 256;
+            p.nchunks = (long)((n + p.C - 1) / p.C);
+            p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks), q->device);
+            p.hist = q->hist[sl].p;
+            p.H = spec ? (int)hl : 0;
+            if (!spec) q->ord.wait(e.stream);         // chunks near the start read the true state
+            k::agc_spec_front(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
+        }
+        if (n > 0) k::delay_hist(dx, q->hist[sl].p, q->hist[1 - sl].p, n, (int)hl, e.stream);
+        q->front.mark(e.stream);
+        q->ord.wait(e.stream);
         if (n > 0) {
-            // exact warm-up W = 20/bandwidth after an approximate one of Wa = 40/bandwidth
-            // (k_agc.hip); measured on the AM chain at bandwidth 0.01 the exact loop then
-            // coalesces within ~110 samples on average, 2834 at worst.
-            const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
-            static const float wmul = std::getenv("LDSP_AGC_WMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WMUL")) : 20.0f;
-            static const float wamul = std::getenv("LDSP_AGC_WAMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WAMUL")) : 40.0f;
-            static const int rounds = std::getenv("LDSP_AGC_ROUNDS") ? std::atoi(std::getenv("LDSP_AGC_ROUNDS")) : 3;
-            const int W = (int)std::min(1 << 18, std::max(256, (int)(wmul / a)));
-            const int Wa = (int)std::min(1 << 20, std::max(1024, (int)(wamul / a)));
-            if (n >= (size_t)4 * (W + Wa)) {
-                k::SpecPlan p;
-                p.W = W;
-                p.Wa = Wa;
-                p.rounds = std::max(0, std::min(rounds, 6));
-                p.C = 256;
-                p.nchunks = (long)((n + p.C - 1) / p.C);
-                p.scratch = q->scratch.ensure(k::agc_scratch_bytes(p.nchunks), q->device);
+            if (par) {
                 static const bool dbg = std::getenv("LDSP_DEBUG_AGC") != nullptr;
                 if (dbg) {
                     p.dbg = (unsigned*)p.scratch + (size_t)p.nchunks * 8;
                     LDSP_HIP(hipMemsetAsync(p.dbg, 0, 8 * sizeof(unsigned), e.stream));
                 }
-                k::agc_spec(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
+                k::agc_spec_back(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
                 if (dbg) {
                     unsigned c[8];
                     LDSP_HIP(hipMemcpyAsync(c, p.dbg, sizeof(c), hipMemcpyDeviceToHost, e.stream));
                     LDSP_HIP(hipStreamSynchronize(e.stream));
-                    std::fprintf(stderr, "[ldsp agc] n=%zu chunks=%ld W=%d Wa=%d rounds=%d reruns per round:", n, p.nchunks,
-                                 p.W, p.Wa, p.rounds);
+                    std::fprintf(stderr, "[ldsp agc] n=%zu chunks=%ld W=%d Wa=%d spec=%d rounds=%d reruns per round:", n,
+                                 p.nchunks, p.W, p.Wa, spec ? 1 : 0, p.rounds);
                     for (int r = 0; r <= p.rounds; r++) std::fprintf(stderr, " %u", c[r]);
                     std::fprintf(stderr, " (last = verifier)\n");
                 }
@@ -1549,8 +1583,11 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
                 k::agc_seq(dx, n, q->dst.as<k::AgcState>(), dy, dstat, e.stream);
             }
             q->dev_newer = true;
+            q->hist_valid = std::min<long>(hl, q->hist_valid + (long)n);
         }
         q->ord.mark(e.stream);
+        q->slot[sl].mark(e.stream);
+        q->ncall++;
         q->last = e.stream;
         if (status && n > 0) {
             LDSP_HIP(hipMemcpyAsync(status, dstat, n, hipMemcpyDeviceToHost, e.stream));

@@ -30,6 +30,15 @@ struct AgcReg {
 };
 
 __device__ __forceinline__ float ldnt(const float* p) { return __builtin_nontemporal_load(p); }
+
+// Input extended by the previous call's last H samples: x[i] for i >= 0,
+// hist[H + i] for -H <= i < 0 (history kept for the speculative warm-ups).
+struct XExt {
+    const float2* x;
+    const float2* hist;
+    long H;
+    __device__ __forceinline__ float2 operator[](long i) const { return i >= 0 ? x[i] : hist[H + i]; }
+};
 __device__ __forceinline__ unsigned ldntu(const unsigned* p) { return __builtin_nontemporal_load(p); }
 
 // AGC(_squelch_update_mode)
@@ -103,8 +112,8 @@ __device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, fl
     }
 }
 
-__device__ __forceinline__ void agc_run_approx(AgcReg& r, const AgcState& p, const float2* __restrict__ x, long a,
-                                               long b)
+template <class X>
+__device__ __forceinline__ void agc_run_approx(AgcReg& r, const AgcState& p, const X& x, long a, long b)
 {
     constexpr int kA = 8;
     for (long i = a; i < b; i += kA) {
@@ -120,8 +129,8 @@ __device__ __forceinline__ void agc_run_approx(AgcReg& r, const AgcState& p, con
 // Run the AGC over x[a, b) with the loads software-pipelined kB samples ahead
 // (they are off the gain recurrence's dependence chain).  OUT: write y/status.
 constexpr int kB = 8;
-template <bool OUT>
-__device__ __forceinline__ void agc_run(AgcReg& r, const AgcState& p, const float2* __restrict__ x, long a, long b,
+template <bool OUT, class X>
+__device__ __forceinline__ void agc_run(AgcReg& r, const AgcState& p, const X& x, long a, long b,
                                         float2* __restrict__ y, uint8_t* __restrict__ status)
 {
     if (a >= b) return;
@@ -172,24 +181,31 @@ __global__ void k_agc_seq(const float2* __restrict__ x, long n, AgcState* st, fl
 // guess within a few ulps of the true trajectory, so the exact float32 loop
 // coalesces bit for bit within ~100 samples typically (a few thousand at
 // worst; chunks that have not are re-run by k_agc_runfix / k_agc_verify).
-constexpr int kPow = 256;
-__global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x, long n, const AgcState* st, int C,
-                                                   int W, int Wa, long nch, unsigned* __restrict__ sc,
-                                                   float2* __restrict__ y, uint8_t* __restrict__ status)
+constexpr int kPow = kAgcPow;
+// H > 0 (speculative call): the H samples before x[0] come from hist and every
+// chunk, chunk 0 included, starts from a guess (H >= W + Wa + kPow), so the
+// kernel never reads the true state and may overlap the previous call's
+// back half; chunk 0 is then checked against the true state like any other.
+__global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x, const float2* __restrict__ hist, long H,
+                                                   long n, const AgcState* st, int C, int W, int Wa, long nch,
+                                                   unsigned* __restrict__ sc, float2* __restrict__ y,
+                                                   uint8_t* __restrict__ status)
 {
     const long chunk = (long)blockIdx.x * 64 + threadIdx.x;
     if (chunk >= nch) return;
     const AgcState p = *st;
+    const XExt xe{x, hist, H};
+    const long lo = -H;                  // earliest sample available
     const long s0 = chunk * C, s1 = min(n, s0 + C);
     long w0 = s0 - W;
     AgcReg r;
-    if (w0 <= 0) {
-        w0 = 0;
+    if (w0 <= lo) {
+        w0 = lo;
         r = AgcReg{p.g, p.y2p, p.mode, p.timer};
     } else {
         long a0 = w0 - Wa;
-        if (a0 <= 0) {
-            a0 = 0;
+        if (a0 <= lo) {
+            a0 = lo;
             r = AgcReg{p.g, p.y2p, p.mode, p.timer};
         } else {
             r.y2p = 1.0f;
@@ -198,7 +214,7 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
             if (p.locked) {
                 r.g = p.g;                          // gain frozen while locked
             } else {
-                const long a = max(0L, a0 - kPow);
+                const long a = max(lo, a0 - kPow);
                 const long m = a0 - a;
                 double pw = 0.0;
                 if (m > 0) {
@@ -206,7 +222,7 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
                     for (long i = a; i < a0; i += 16) {
                         float2 v[16];
 #pragma unroll
-                        for (int j = 0; j < 16; j++) v[j] = x[min(i + j, a0 - 1)];
+                        for (int j = 0; j < 16; j++) v[j] = xe[min(i + j, a0 - 1)];
 #pragma unroll
                         for (int j = 0; j < 16; j++)
                             if (i + j < a0) acc[j & 3] += (double)v[j].x * v[j].x + (double)v[j].y * v[j].y;
@@ -217,9 +233,9 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
                 r.g = (float)(g > 1e6 ? 1e6 : g);
             }
         }
-        agc_run_approx(r, p, x, a0, w0);
+        agc_run_approx(r, p, xe, a0, w0);
     }
-    agc_run<false>(r, p, x, w0, s0, y, status);
+    agc_run<false>(r, p, xe, w0, s0, y, status);
     unsigned* gs = sc + chunk * 8;
     gs[0] = __float_as_uint(r.g);
     gs[1] = __float_as_uint(r.y2p);
@@ -242,6 +258,15 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
 // start, whose own thread began from a stale state: the next flags pass
 // catches that.  One round replaces the ~R/2 parity rounds a run of R failed
 // chunks needed.
+// End state (g, y2p, mode, timer) of chunk k - 1; for chunk 0 of a
+// speculative call, the true state the previous call left in st.
+__device__ __forceinline__ unsigned pred_word(const unsigned* sc, const AgcState* st, long k, int i)
+{
+    if (k > 0) return ldntu(sc + (k - 1) * 8 + 4 + i);
+    const unsigned* w = (const unsigned*)st;
+    return ldntu(w + (i == 0 ? 0 : i == 1 ? 1 : i == 2 ? 5 : 6));
+}
+
 __device__ __forceinline__ bool agc_flag(const unsigned long long* flags, long c)
 {
     return (flags[c >> 6] >> (c & 63)) & 1ull;
@@ -253,10 +278,10 @@ __global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x,
                                                    float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg)
 {
     const long k = (long)blockIdx.x * 64 + threadIdx.x;
-    if (k < 1 || k >= nch || !agc_flag(flags, k) || agc_flag(flags, k - 1)) return;
+    if (k >= nch || !agc_flag(flags, k) || (k > 0 && agc_flag(flags, k - 1))) return;
     const AgcState p = *st;
-    const unsigned* pe = sc + (k - 1) * 8 + 4;
-    AgcReg r{__uint_as_float(ldntu(pe)), __uint_as_float(ldntu(pe + 1)), (int)ldntu(pe + 2), ldntu(pe + 3)};
+    AgcReg r{__uint_as_float(pred_word(sc, st, k, 0)), __uint_as_float(pred_word(sc, st, k, 1)),
+             (int)pred_word(sc, st, k, 2), pred_word(sc, st, k, 3)};
     bool inrun = true;
     for (long m = k; m < nch; m++) {
         unsigned* gs = sc + m * 8;
@@ -286,34 +311,35 @@ __global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x,
 
 // Parallel pre-check: bit c of flags[c / 64] = chunk c's start state differs
 // from chunk c-1's end state (after the repair rounds).
+// spec: every chunk started from a guess (chunk 0 is compared with the true state).
 __global__ void __launch_bounds__(64) k_agc_flags(int C, int W, long nch, const unsigned* __restrict__ sc,
-                                                  unsigned long long* __restrict__ flags)
+                                                  const AgcState* st, int spec, unsigned long long* __restrict__ flags)
 {
     const long kk = (long)blockIdx.x * 64 + threadIdx.x;
     bool bad = false;
-    if (kk >= 1 && kk < nch && kk * C - W > 0) {
+    if (kk < nch && (spec ? true : (kk >= 1 && kk * C - W > 0))) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) bad |= sc[kk * 8 + i] != sc[(kk - 1) * 8 + 4 + i];
+        for (int i = 0; i < 4; i++) bad |= sc[kk * 8 + i] != pred_word(sc, st, kk, i);
     }
     const unsigned long long m = __ballot(bad);
     if (threadIdx.x == 0) flags[blockIdx.x] = m;
 }
 
 __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x, long n, AgcState* st, int C, int W,
-                                                   long nch, unsigned* __restrict__ sc,
+                                                   int spec, long nch, unsigned* __restrict__ sc,
                                                    const unsigned long long* __restrict__ flags, float2* __restrict__ y,
                                                    uint8_t* __restrict__ status, unsigned* dbg)
 {
     const int lane = threadIdx.x;
     const AgcState p = *st;
     const long nw = (nch + 63) / 64;
-    long k = 1;
+    long k = spec ? 0 : 1;
     bool direct = false;          // chunk k's predecessor was re-run: compare states, not its flag
     while (k < nch) {
         long kb;
         if (direct) {
             bool bad = false;
-            if (k * C - W > 0 && lane < 4) bad = ldntu(sc + k * 8 + lane) != ldntu(sc + (k - 1) * 8 + 4 + lane);
+            if ((spec || k * C - W > 0) && lane < 4) bad = ldntu(sc + k * 8 + lane) != pred_word(sc, st, k, lane);
             if (__ballot(bad) == 0) {
                 direct = false;
                 k++;
@@ -338,8 +364,8 @@ __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x,
             if (kb >= nch) break;
         }
         if (lane == 0) {
-            const unsigned* e = sc + (kb - 1) * 8 + 4;
-            AgcReg r{__uint_as_float(ldntu(e)), __uint_as_float(ldntu(e + 1)), (int)ldntu(e + 2), ldntu(e + 3)};
+            AgcReg r{__uint_as_float(pred_word(sc, st, kb, 0)), __uint_as_float(pred_word(sc, st, kb, 1)),
+                     (int)pred_word(sc, st, kb, 2), pred_word(sc, st, kb, 3)};
             agc_run<true>(r, p, x, kb * C, min(n, kb * C + C), y, status);
             if (dbg) dbg[0]++;
             unsigned* en = sc + kb * 8;
@@ -394,23 +420,29 @@ void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hi
 size_t agc_flags_offset_words(long nchunks) { return (size_t)nchunks * 8 + 8; }     // after records + debug words
 size_t agc_scratch_bytes(long nchunks) { return (agc_flags_offset_words(nchunks) + 2 * ((nchunks + 63) / 64 + 64)) * 4; }
 
-void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
+void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
     {
         LDSP_PROF(s, "k_agc_chunks");
         hipLaunchKernelGGL(k_agc_chunks, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, (const float2*)x,
-                           (long)n, (const AgcState*)st, p.C, p.W, p.Wa, p.nchunks, (unsigned*)p.scratch, (float2*)y,
-                           status);
+                           (const float2*)p.hist, (long)p.H, (long)n, (const AgcState*)st, p.C, p.W, p.Wa, p.nchunks,
+                           (unsigned*)p.scratch, (float2*)y, status);
     }
     LDSP_HIP(hipGetLastError());
+}
+
+void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
+{
+    if (n == 0) return;
+    const int spec = p.H > 0 ? 1 : 0;
     unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
     const unsigned nb = (unsigned)((p.nchunks + 63) / 64);
     for (int round = 0; round <= p.rounds; round++) {
         {
             LDSP_PROF(s, "k_agc_flags");
             hipLaunchKernelGGL(k_agc_flags, dim3(nb), dim3(64), 0, s, p.C, p.W, p.nchunks, (const unsigned*)p.scratch,
-                               flags);
+                               (const AgcState*)st, spec, flags);
         }
         LDSP_HIP(hipGetLastError());
         if (round == p.rounds) break;
@@ -424,8 +456,8 @@ void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y,
     }
     {
         LDSP_PROF(s, "k_agc_verify");
-        hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, p.nchunks,
-                           (unsigned*)p.scratch, (const unsigned long long*)flags, (float2*)y, status,
+        hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, spec,
+                           p.nchunks, (unsigned*)p.scratch, (const unsigned long long*)flags, (float2*)y, status,
                            p.dbg ? p.dbg + p.rounds : nullptr);
     }
     LDSP_HIP(hipGetLastError());

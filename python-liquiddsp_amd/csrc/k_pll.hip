@@ -714,6 +714,17 @@ size_t pll_scratch_bytes(size_t n) { return pll_layout(n).total; }
 
 size_t pll_stats_offset(size_t n) { return pll_layout(n).stats; }
 
+void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m, hipStream_t s)
+{
+    if (m <= 0) return;
+    {
+        LDSP_PROF(s, "k_delay_hist");
+        hipLaunchKernelGGL(k_delay_hist, dim3(1), dim3(256), 0, s, (const float2*)x, (const float2*)hist,
+                           (float2*)hist_out, (long)n, m);
+    }
+    LDSP_HIP(hipGetLastError());
+}
+
 bool pll_parallel(size_t n) { return n >= (size_t)4 * kWarm; }
 
 static PllIn pll_in(const PllCall& c)

@@ -111,6 +111,8 @@ struct SpecPlan {
     unsigned* dbg = nullptr;   // AGC debug: per-round re-run counters (LDSP_DEBUG_AGC)
     long nchunks;
     void* scratch;        // device scratch (states: start-guess and end per chunk)
+    const void* hist = nullptr;   // AGC: the H input samples before x[0] (H > 0: every chunk speculative)
+    int H = 0;
 };
 // scratch for iir_spec: chunk states + verifier flag words
 size_t spec_flags_offset(long nchunks, int ncomp, int fs);
@@ -126,10 +128,19 @@ struct AgcState {         // device-resident agc_crcf state
     float threshold;
     int pad[3];
 };
+constexpr int kAgcPow = 256;     // samples whose mean power sets a chunk's guessed gain
 void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hipStream_t s);
 size_t agc_scratch_bytes(long nchunks);
-void agc_spec(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
-              hipStream_t s);
+// Chunk-parallel exact AGC in two halves.  Front: the chunks (reads only the
+// parameters when p.H > 0, so it may run while the previous call's back half
+// still advances the state).  Back: flag / repair rounds and the verifier
+// against the true state, which it then advances.
+void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
+                    hipStream_t s);
+void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
+                   hipStream_t s);
+// hist_out = the last m samples of (hist, x[0, n)) (complex), for the next call.
+void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m, hipStream_t s);
 
 // ------------------------------------------------------------------ AmpModem
 struct AmpState {         // device-resident PLL state

@@ -363,6 +363,37 @@ def test_agc_bitwise(ld, ora, rng, n):
     assert np.float32(g.gain) == np.float32(o.gain)
 
 
+def test_agc_speculative_calls_on_two_streams(ld, ora, rng):
+    # Calls of >= 4 (W + Wa) samples whose predecessor left a full input history
+    # run every chunk from a guess (k_agc_chunks with H > 0), overlapping the
+    # previous call's back half on the other stream; chunk 0 is checked against
+    # the true state.  Short calls take the sequential path but still feed the
+    # history; reset() keeps the history and restarts the state.
+    import torch
+    x = _am(rng, 260_000, 48000.0, 300.0)
+    g = ld.AGC()
+    g.lock = False
+    g.scale = 0.01
+    o = ora.AGC()
+    o.scale = np.float32(0.01)
+    xd = torch.from_numpy(x).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    cuts = [0, 30_000, 60_000, 65_000, 95_000, 125_000, 155_000, 200_000, 260_000]
+    outs, refs = [], []
+    for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        if i == 6:
+            torch.cuda.synchronize()
+            g.reset()
+            o.reset()
+        with torch.cuda.stream(streams[i % 2]):
+            outs.append(g(xd[a:b]))
+        refs.append(o(x[a:b]))
+    torch.cuda.synchronize()
+    assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), np.concatenate(refs))
+    assert np.float32(g.gain) == np.float32(o.gain)
+
+
 def test_agc_squelch_and_onrise(ld, ora, rng):
     quiet = cgauss(rng, 4000, 1e-3)
     loud = cgauss(rng, 4000, 1.0)
