@@ -1699,12 +1699,13 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     k::pll_back(c, e.stream);
     if (!par) q->front.mark(e.stream);
     if (par && std::getenv("LDSP_DEBUG_PLL")) {
-        unsigned long long stt[5];
+        unsigned long long stt[7];
         LDSP_HIP(hipMemcpyAsync(stt, (char*)c.scratch + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
                                 e.stream));
         LDSP_HIP(hipStreamSynchronize(e.stream));
         std::fprintf(stderr, "[ldsp pll] n=%zu entries=%llu repairs=%llu fallback_lane_blocks=%llu walk_clk=%llu "
-                     "wait_clk=%llu\n", n, stt[4], stt[0], stt[1], stt[2], stt[3]);
+                     "wait_clk=%llu lane_blocks_repaired=%llu first_pass_set_final=%llu\n", n, stt[4], stt[0], stt[1],
+                     stt[2], stt[3], stt[5], stt[6]);
     }
     return mbuf;
 }

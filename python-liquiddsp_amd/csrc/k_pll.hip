@@ -136,7 +136,7 @@ struct CandBuf {
     unsigned long long* stats;   // walker counters (LDSP_DEBUG_PLL)
     long nchc;
     uint32_t B;           // risky margin (table-cell units of 2^-22)
-    int dbg;              // 0; 1 counters; 2 counters + every lane-block through the generic path
+    int dbg;              // 0; 1 counters; 2 counters + every lane-block through the generic path; 3 no repairs (timing)
 };
 
 __device__ __forceinline__ bool risky(uint32_t w, uint32_t B) { return ((w + B) & 0x3fffffu) < 2u * B; }
@@ -476,7 +476,7 @@ __device__ __forceinline__ uint32_t sel_lane(uint32_t pout, uint32_t so, unsigne
 
 // Walker state (wave-uniform): f(s) = Kb + (s - S) D + A(s), S = the current walker block's sample base.
 struct WState {
-    uint32_t Kb, D, nrep, nfb;
+    uint32_t Kb, D, nrep, nfb, nlb, nsame;
 };
 
 // Generic walk of every sample in [sa, sb]: 64 consecutive samples per step,
@@ -530,22 +530,33 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
     unsigned long long mask = __builtin_amdgcn_ballot_w64(x > E0.y);
     const long s_last = (long)S + rl(srel, nv - 1);
     if (STATS && cb.dbg == 2) mask = 1;
+    if (STATS && cb.dbg == 3) mask = 0;      // timing only: no repairs (wrong output)
+    const unsigned long long mask0 = mask;
     if (mask != 0) {
         const WState g0 = g;
-        uint32_t Kb = g.Kb, D = g.D;
+        uint32_t Kb = rfl(g.Kb), D = rfl(g.D);       // scalar accumulators
         uint32_t xpost = 0;
         unsigned long long PM = 0;
-        do {
-            const int j = __builtin_ctzll(mask);
-            const uint32_t dk1 = rl(E1.x, j), dk2p = rl(E1.y, j);
-            const unsigned long long bit = 1ull << j;
-            PM |= bit;
-            x = mad_lane<F24>(sx, dk1, x) + dk2p;
-            xpost = sel_lane(xpost, x, bit);
-            D += dk1;
-            Kb += dk2p;
-            mask = __builtin_amdgcn_ballot_w64(x > E0.y) & ((~0ull << j) << 1);
-        } while (mask != 0);
+        // two repairs per loop trip: the back branch is taken every other repair
+#define LDSP_WALK_REPAIR                                                                   \
+    {                                                                                      \
+        const int j = __builtin_ctzll(mask);                                               \
+        const uint32_t dk1 = rl(E1.x, j), dk2p = rl(E1.y, j);                              \
+        const unsigned long long bit = 1ull << j;                                          \
+        PM |= bit;                                                                         \
+        x = mad_lane<F24>(sx, dk1, x) + dk2p;                                              \
+        xpost = sel_lane(xpost, x, bit);                                                   \
+        D += dk1;                                                                          \
+        Kb += dk2p;                                                                        \
+        mask = __builtin_amdgcn_ballot_w64(x > E0.y) & ((~0ull << j) << 1);                \
+    }
+        while (true) {
+            LDSP_WALK_REPAIR
+            if (mask == 0) break;
+            LDSP_WALK_REPAIR
+            if (mask == 0) break;
+        }
+#undef LDSP_WALK_REPAIR
         const uint32_t twoB = 2u * cb.B;
         const uint32_t xpre = xpost - mad_lane<F24>(sx, E1.x, E1.y);      // x_post - dk2
         const unsigned long long FL = __builtin_amdgcn_ballot_w64(E0.z & (1u << 28));
@@ -567,7 +578,11 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
             if ((PM >> lane) & 1ull) y[(long)S + srel] = __uint_as_float(E1.z);
             g.Kb = Kb;
             g.D = D;
-            if (STATS) g.nrep += (unsigned)__builtin_popcountll(PM);
+            if (STATS) {
+                g.nrep += (unsigned)__builtin_popcountll(PM);
+                g.nlb++;
+                g.nsame += PM == mask0 ? 1u : 0u;
+            }
         }
     }
     s_next = s_last + 1;
@@ -611,6 +626,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     g.D = st->dtheta - cb.cs[1];
     g.nrep = 0;
     g.nfb = 0;
+    g.nlb = 0;
+    g.nsame = 0;
     uint32_t S = 0;
     long s_next = 0;
     unsigned long long cyc_walk = 0, cyc_wait = 0;
@@ -666,6 +683,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             cb.stats[2] = cyc_walk;
             cb.stats[3] = cyc_wait;
             cb.stats[4] = NE;
+            cb.stats[5] = g.nlb;
+            cb.stats[6] = g.nsame;
         }
     }
 }

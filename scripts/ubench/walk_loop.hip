@@ -1,0 +1,112 @@
+// Microbenchmark of the PLL walker's repair loop on gfx950: every lane of every
+// lane-block is an event (W = 0), so each lane-block runs 64 dependent repairs.
+// Reports device cycles (s_memtime) per repair for loop variants.
+//   hipcc --offload-arch=gfx950 -O3 walk_loop.hip -o walk_loop && ./walk_loop
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
+__device__ __forceinline__ uint32_t sel_lane(uint32_t a, uint32_t b, unsigned long long bit)
+{
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(bit));
+    return r;
+}
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t s, uint32_t v)
+{
+    uint32_t r;
+    asm volatile("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(s), "v"(v));
+    return r;
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) k_loop(const uint4* E, uint32_t* out, int nlb, unsigned long long* clk)
+{
+    const int lane = threadIdx.x;
+    const uint4 e = E[lane];
+    uint32_t x = e.x, W = 0, sx = e.w & 0xffff, d1 = e.y & 0xfff, d2 = e.z;
+    uint32_t Kb = 0, D = 0, xpost = 0, acc = 0;
+    unsigned long long PM = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int b = 0; b < nlb; b++) {
+        unsigned long long mask = __builtin_amdgcn_ballot_w64(x + b > W);
+        if (V == 0) {            // the walker's loop
+            do {
+                const int j = __builtin_ctzll(mask);
+                const uint32_t dk1 = rl(d1, j), dk2p = rl(d2, j);
+                const unsigned long long bit = 1ull << j;
+                PM |= bit;
+                x = mad24(sx, dk1, x) + dk2p;
+                xpost = sel_lane(xpost, x, bit);
+                D += dk1;
+                Kb += dk2p;
+                mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
+            } while (mask != 0);
+        } else if (V == 1) {     // minimal chain: no snapshot, no accumulators
+            do {
+                const int j = __builtin_ctzll(mask);
+                const uint32_t dk1 = rl(d1, j), dk2p = rl(d2, j);
+                x = mad24(sx, dk1, x) + dk2p;
+                mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
+            } while (mask != 0);
+        } else if (V == 2) {     // no readlane: scalar operands from ff1 only
+            do {
+                const int j = __builtin_ctzll(mask);
+                x = mad24(sx, (uint32_t)j, x) + (uint32_t)j;
+                mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
+            } while (mask != 0);
+        } else if (V == 3) {     // pure SALU loop over the mask (no ballot per step)
+            do {
+                const int j = __builtin_ctzll(mask);
+                const uint32_t dk1 = rl(d1, j), dk2p = rl(d2, j);
+                x = mad24(sx, dk1, x) + dk2p;
+                mask &= mask - 1;
+            } while (mask != 0);
+        }
+        acc += x;
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[lane] = acc + xpost + Kb + D + (uint32_t)PM;
+    if (lane == 0) *clk = t1 - t0;
+}
+
+int main()
+{
+    uint4 h[64];
+    for (int i = 0; i < 64; i++) h[i] = make_uint4(1000u + 17u * i, 3u + i, 7u * i, i);
+    uint4* dE;
+    uint32_t* dout;
+    unsigned long long* dclk;
+    hipMalloc(&dE, sizeof(h));
+    hipMalloc(&dout, 256);
+    hipMalloc(&dclk, 8);
+    hipMemcpy(dE, h, sizeof(h), hipMemcpyHostToDevice);
+    const int nlb = 2000;
+    auto run = [&](auto kern, const char* name) {
+        for (int rep = 0; rep < 2; rep++) hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, 0, dE, dout, nlb, dclk);
+        hipDeviceSynchronize();
+        unsigned long long c = 0;
+        hipMemcpy(&c, dclk, 8, hipMemcpyDeviceToHost);
+        printf("%-40s %8.1f memtime ticks per repair (x %d repairs)\n", name, (double)c / (64.0 * nlb), 64 * nlb);
+    };
+    run(k_loop<0>, "V0 walker loop");
+    run(k_loop<1>, "V1 minimal chain");
+    run(k_loop<2>, "V2 no readlane");
+    run(k_loop<3>, "V3 no ballot (SALU mask walk)");
+    // s_memtime frequency: compare against wall clock
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(k_loop<0>, dim3(1), dim3(64), 0, 0, dE, dout, nlb * 10, dclk);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    unsigned long long c = 0;
+    hipMemcpy(&c, dclk, 8, hipMemcpyDeviceToHost);
+    printf("V0 x10: %.3f ms wall, %llu ticks -> %.1f MHz memtime; %.2f ns per repair\n", ms, c, c / (ms * 1e3),
+           ms * 1e6 / (64.0 * nlb * 10));
+    return 0;
+}
