@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 tag=${1:-r01}
 out=gpurun_out/prof/$tag
 mkdir -p $out
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-components"
+B="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-components"
 F="python3 scripts/firbench.py"
 run() {   # name, rocprof args..., -- cmd
   local name=$1; shift
