@@ -595,6 +595,10 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                                                            float* __restrict__ y)
 {
     __shared__ WalkBufE buf[4];          // ring: block c in buf[c & 3], DMA'd three blocks ahead
+    // Own the CU: 8 waves x 256 VGPRs fill every SIMD's register file, so no wave of
+    // the kernels running beside the walk (the next call's AGC, candidates, ...)
+    // is placed on the walker's SIMD and takes issue slots from its serial chain.
+    asm volatile("" ::: "v255");
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: keeps the walk on SALU
     const int lane = tid & 63;
