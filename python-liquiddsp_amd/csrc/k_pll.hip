@@ -315,13 +315,13 @@ __global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb)
 
 // Entry records, one wave per chunk (4 samples per lane).  Per entry (SoA per
 // walker block: E0[kBlkE], E1[kBlkE]), with srel = s - S_blk (< 2^17):
-//   E0 = (c, W, srel | lne << 28 | rne << 29, g)
+//   E0 = (c, W, srel, L')
 //        x = c + Kb + srel D = f(s) - lo; event iff x > W, [lo, lo + W] being
 //        the no-repair interval of f cut to [-B, B] when a neighbouring gap is
-//        non-empty (lne / rne: the gap to the previous / next entry); g = lo + B
-//   E1 = (dk1, dk2 - srel dk1, out, a) for the one crossing direction possible
-//        while |f| < 2^21 (up if u >= 2^21, else down); the crossing really was
-//        that one cell iff x_pre - a < 2^22.
+//        non-empty (the gap to the previous / next entry)
+//   E1 = (dk1, dk2 - srel dk1, out, span) for the one crossing direction possible
+//        while |f| < 2^21 (up if u >= 2^21, else down); the repair was right iff
+//        x_post - L' <= span (see below).
 // The tail of the last walker block is padded with W = ~0 (never an event).
 __global__ void __launch_bounds__(256) k_pll_entries(CandBuf cb, long n)
 {
@@ -363,15 +363,30 @@ __global__ void __launch_bounds__(256) k_pll_entries(CandBuf cb, long n)
             lo = max(lo, -B);
             hi = min(hi, B);
         }
-        const uint32_t z = u + (uint32_t)lo;       // v = u + f = x + z
         const bool up = u >= (1u << 21);
         const uint32_t dk1 = up ? R0[r].w : R0[r].y, dk2 = up ? R1[r].x : R0[r].z;
         const uint32_t out = up ? R1[r].z : R1[r].y;
-        const uint32_t a = up ? (1u << 22) - z : 0u - (1u << 22) - z;
+        // A repair here is right iff f_pre (the offset before it) lies in the
+        // intersection of: the presumed one-cell crossing, [-B, B] if the left gap
+        // is non-empty, and [-B - dk2, B - dk2] (f_post within B) if the right one
+        // is.  All three are small signed intervals, so their intersection is one,
+        // checked on the walker's snapshot x_post = f_pre - lo + dk2.
+        long fl = up ? (1l << 22) - (long)u : -(1l << 22) - (long)u;
+        long fh = fl + (1l << 22) - 1;
+        if (lne) {
+            fl = max(fl, (long)-B);
+            fh = min(fh, (long)B);
+        }
+        if (rne) {
+            const long d2 = (long)(int)dk2;
+            fl = max(fl, -(long)B - d2);
+            fh = min(fh, (long)B - d2);
+        }
+        const uint32_t Lp = fl <= fh ? (uint32_t)(fl - lo) + dk2 : 0x80000000u;   // empty: always redo
+        const uint32_t span = fl <= fh ? (uint32_t)(fh - fl) : 0u;
         uint4* E = cb.ent + (size_t)blk * 2 * kBlkE;
-        E[idx] = make_uint4(A - (uint32_t)lo, (uint32_t)(hi - lo), srel | (lne ? 1u << 28 : 0u) | (rne ? 1u << 29 : 0u),
-                            (uint32_t)lo + (uint32_t)B);
-        E[kBlkE + idx] = make_uint4(dk1, dk2 - srel * dk1, out, a);
+        E[idx] = make_uint4(A - (uint32_t)lo, (uint32_t)(hi - lo), srel, Lp);
+        E[kBlkE + idx] = make_uint4(dk1, dk2 - srel * dk1, out, span);
     }
     if (k == cb.nchc - 1) {              // pad the last walker block: events never fire there
         const uint32_t ne = e, end = (ne + kBlkE - 1) / kBlkE * kBlkE;
@@ -520,15 +535,23 @@ __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_
 // gap is non-empty and f_post within B where the right gap is; else the
 // lane-block is redone by walk_fallback from its saved state.  The repaired
 // outputs are stored only then.
+// Where the previous lane-block ended (its srel register, valid lanes and
+// block base): the first sample a fallback of this lane-block must redo.  Only
+// read on that rare path, so no lane-block waits for a readlane.
+struct PrevLB {
+    uint32_t srel;
+    int nv;
+    uint32_t S;
+    bool first;
+};
+
 template <bool F24, bool STATS>
-__device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv, WState& g, uint32_t S, long& s_next,
+__device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv, WState& g, uint32_t S, PrevLB& prev,
                                         const CandBuf& cb, const FullCtx& fc, float* y, int lane)
 {
-    const uint32_t srel = E0.z & 0xffffffu;
-    const uint32_t sx = F24 ? E0.z : srel;          // v_mad_i32_i24 reads the low 24 bits only
+    const uint32_t srel = E0.z, sx = srel;
     uint32_t x = E0.x + g.Kb + srel * g.D;
     unsigned long long mask = __builtin_amdgcn_ballot_w64(x > E0.y);
-    const long s_last = (long)S + rl(srel, nv - 1);
     if (STATS && cb.dbg == 2) mask = 1;
     if (STATS && cb.dbg == 3) mask = 0;      // timing only: no repairs (wrong output)
     const unsigned long long mask0 = mask;
@@ -537,45 +560,67 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
         uint32_t Kb = rfl(g.Kb), D = rfl(g.D);       // scalar accumulators
         uint32_t xpost = 0;
         unsigned long long PM = 0;
-        // two repairs per loop trip: the back branch is taken every other repair
-#define LDSP_WALK_REPAIR                                                                   \
-    {                                                                                      \
-        const int j = __builtin_ctzll(mask);                                               \
-        const uint32_t dk1 = rl(E1.x, j), dk2p = rl(E1.y, j);                              \
-        const unsigned long long bit = 1ull << j;                                          \
-        PM |= bit;                                                                         \
-        x = mad_lane<F24>(sx, dk1, x) + dk2p;                                              \
-        xpost = sel_lane(xpost, x, bit);                                                   \
-        D += dk1;                                                                          \
-        Kb += dk2p;                                                                        \
-        mask = __builtin_amdgcn_ballot_w64(x > E0.y) & ((~0ull << j) << 1);                \
-    }
-        while (true) {
-            LDSP_WALK_REPAIR
-            if (mask == 0) break;
-            LDSP_WALK_REPAIR
-            if (mask == 0) break;
+        if (F24) {
+            // The repair chain, hand-scheduled (15 instructions; s_and sets SCC for
+            // the back branch, no s_cmp): per repair j = ff1(mask); dk1, dk2' =
+            // lane j's (readlane); x += dk2' + srel dk1 in every lane; snapshot
+            // lane j's x; mask = events after j.  Exec is the full wave here.
+            uint32_t j, dk1, dk2;
+            unsigned long long bit, above;
+            asm volatile(
+                "1:\n\t"
+                "s_ff1_i32_b64 %[j], %[mask]\n\t"
+                "v_readlane_b32 %[dk1], %[e1x], %[j]\n\t"
+                "v_readlane_b32 %[dk2], %[e1y], %[j]\n\t"
+                "s_lshl_b64 %[bit], 1, %[j]\n\t"
+                "s_lshl_b64 %[above], -2, %[j]\n\t"
+                "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+                "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
+                "v_add_u32 %[x], %[dk2], %[x]\n\t"
+                "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
+                "s_add_u32 %[d], %[d], %[dk1]\n\t"
+                "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
+                "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
+                "s_and_b64 %[mask], %[mask], %[above]\n\t"
+                "s_cbranch_scc1 1b"
+                : [x] "+v"(x), [xp] "+v"(xpost), [mask] "+s"(mask), [pm] "+s"(PM), [kb] "+s"(Kb), [d] "+s"(D),
+                  [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [bit] "=&s"(bit), [above] "=&s"(above)
+                : [e1x] "v"(E1.x), [e1y] "v"(E1.y), [sx] "v"(sx), [w] "v"(E0.y)
+                : "scc");
+        } else {
+            do {
+                const int j = __builtin_ctzll(mask);
+                const uint32_t dk1 = rl(E1.x, j), dk2p = rl(E1.y, j);
+                const unsigned long long bit = 1ull << j;
+                PM |= bit;
+                x = mad_lane<F24>(sx, dk1, x) + dk2p;
+                xpost = sel_lane(xpost, x, bit);
+                D += dk1;
+                Kb += dk2p;
+                mask = __builtin_amdgcn_ballot_w64(x > E0.y) & ((~0ull << j) << 1);
+            } while (mask != 0);
         }
-#undef LDSP_WALK_REPAIR
-        const uint32_t twoB = 2u * cb.B;
-        const uint32_t xpre = xpost - mad_lane<F24>(sx, E1.x, E1.y);      // x_post - dk2
-        const unsigned long long FL = __builtin_amdgcn_ballot_w64(E0.z & (1u << 28));
-        const unsigned long long FR = __builtin_amdgcn_ballot_w64(E0.z & (1u << 29));
-        unsigned long long bad = __builtin_amdgcn_ballot_w64(xpre - E1.w >= (1u << 22));
-        bad |= __builtin_amdgcn_ballot_w64(xpre + E0.w > twoB) & FL;
-        bad |= __builtin_amdgcn_ballot_w64(xpost + E0.w > twoB) & FR;
-        bad &= PM;
+        // every repaired lane: x_post - L' <= span (E0.w, E1.w: k_pll_entries)
+        unsigned long long bad = __builtin_amdgcn_ballot_w64(xpost - E0.w > E1.w) & PM;
         if (STATS && cb.dbg == 2) bad = 1;
         if (__builtin_expect(bad != 0, 0)) {
             WState r = g0;
             r.nfb++;
-            r = walk_fallback(r, s_next, s_last, S, cb, fc, y, lane);
+            const long s_first = prev.first ? 0l : (long)prev.S + rl(prev.srel, prev.nv - 1) + 1;
+            r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, y, lane);
             g.Kb = rfl(r.Kb);
             g.D = rfl(r.D);
             g.nrep = rfl(r.nrep);
             g.nfb = rfl(r.nfb);
         } else {
-            if ((PM >> lane) & 1ull) y[(long)S + srel] = __uint_as_float(E1.z);
+            // store the repaired lanes' outputs with exec = PM
+            float* yb = y + S;
+            asm volatile("s_mov_b64 exec, %[pm]\n\t"
+                         "global_store_dword %[off], %[v], %[base]\n\t"
+                         "s_mov_b64 exec, -1"
+                         :
+                         : [pm] "s"(PM), [off] "v"(srel << 2), [v] "v"(E1.z), [base] "s"(yb)
+                         : "memory", "exec");
             g.Kb = Kb;
             g.D = D;
             if (STATS) {
@@ -585,7 +630,10 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
             }
         }
     }
-    s_next = s_last + 1;
+    prev.srel = srel;
+    prev.nv = nv;
+    prev.S = S;
+    prev.first = false;
 }
 
 // Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + 3
@@ -633,7 +681,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     g.nlb = 0;
     g.nsame = 0;
     uint32_t S = 0;
-    long s_next = 0;
+    PrevLB prev{0u, 1, 0u, true};
     unsigned long long cyc_walk = 0, cyc_wait = 0;
     for (long c = 0; c < nblk; c++) {
         const unsigned long long t0 = STATS ? wall_clock64() : 0;
@@ -658,7 +706,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 const int qn = min(q + 1, kBlkE / 64 - 1) * 64 + lane;
                 const uint4 N0 = b.e[0][qn], N1 = b.e[1][qn];
                 if (q * 64 >= cnt) break;
-                walk_lb<F24, STATS>(A0, A1, min(64, cnt - q * 64), g, S, s_next, cb, fc, y, lane);
+                walk_lb<F24, STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, y, lane);
                 A0 = N0;
                 A1 = N1;
             }

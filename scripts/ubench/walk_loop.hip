@@ -56,6 +56,24 @@ __global__ void __launch_bounds__(64) k_loop(const uint4* E, uint32_t* out, int 
                 x = mad24(sx, (uint32_t)j, x) + (uint32_t)j;
                 mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
             } while (mask != 0);
+        } else if (V == 4) {     // readlane results copied through the SALU before the VALU uses them
+            do {
+                const int j = __builtin_ctzll(mask);
+                uint32_t dk1, dk2p;
+                asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4\n\ts_mov_b32 %0, %0\n\ts_mov_b32 %1, %1"
+                             : "=&s"(dk1), "=&s"(dk2p) : "v"(d1), "v"(d2), "s"(j));
+                x = mad24(sx, dk1, x) + dk2p;
+                mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
+            } while (mask != 0);
+        } else if (V == 5) {     // LDS broadcast of lane j's values into VGPRs (no SGPR hop)
+            __shared__ uint2 tabd[64];
+            tabd[lane] = make_uint2(d1, d2);
+            do {
+                const int j = __builtin_ctzll(mask);
+                const uint2 dd = tabd[j];
+                x = x + sx * dd.x + dd.y;
+                mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
+            } while (mask != 0);
         } else if (V == 3) {     // pure SALU loop over the mask (no ballot per step)
             do {
                 const int j = __builtin_ctzll(mask);
@@ -94,6 +112,8 @@ int main()
     run(k_loop<1>, "V1 minimal chain");
     run(k_loop<2>, "V2 no readlane");
     run(k_loop<3>, "V3 no ballot (SALU mask walk)");
+    run(k_loop<4>, "V4 readlane + s_mov");
+    run(k_loop<5>, "V5 LDS broadcast");
     // s_memtime frequency: compare against wall clock
     hipEvent_t a, b;
     hipEventCreate(&a);
