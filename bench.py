@@ -183,7 +183,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-components", action="store_true")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams the steps rotate over (1 = every step on torch's current stream). "
                          "Each object orders its own calls across streams (libldsp StreamMark), so step k+1's "
                          "IIR/resampler/AGC/candidate kernels overlap step k's serial PLL walk")
