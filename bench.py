@@ -30,6 +30,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# One dependent repair of the PLL walk (ballot -> s_ff1 -> 2 readlanes -> 24-bit
+# multiply-add -> compare), measured alone on MI355X by scripts/ubench/walk_loop.hip
+# (125 shader cycles at 2.4 GHz): the serial floor of the walker per repair.
+REPAIR_FLOOR_NS = 52.2
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector spec
 
 
@@ -282,6 +286,7 @@ def main():
     dom = max(kprof, key=lambda k: kprof[k][1])
     dom_ms = kprof[dom][1] / kprof[dom][0]
     achieved = alg.get(dom, 0) / (dom_ms * 1e-3) / 1e9
+    entries, repairs, fallbacks = radio.am._walk_stats()       # the last call's walk (synchronises)
     res = {
         "metric": "Msamples/s on AM chain (IIR->resample->AGC->demod), 2 MS/s IQ; HBM GB/s vs roofline",
         "value": round(value, 3),
@@ -305,7 +310,11 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("bench", dom),
                      "traffic_source": PMC_SOURCE,
                      "note": "alg bytes = 12 B per PCM sample (AmpModem in + out); the PLL recurrence is "
-                             "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else ""},
+                             "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else "",
+                     "serial_chain": {"entries": int(entries), "repairs": int(repairs), "fallback_lane_blocks": int(fallbacks),
+                                      "floor_ns_per_repair": REPAIR_FLOOR_NS,
+                                      "floor_ms": round(repairs * REPAIR_FLOOR_NS * 1e-6, 4),
+                                      "frac": round(repairs * REPAIR_FLOOR_NS * 1e-6 / dom_ms, 3) if dom_ms else None}},
         "streams": nstreams,
         "host_ms_per_step": round(host_ms, 4),
         "host_ms_max_step": round(host_max_ms, 4),

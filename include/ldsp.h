@@ -216,6 +216,12 @@ int ldsp_ampmodem_reset(ldsp_ampmodem_t q);
 int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t *theta, uint32_t *dtheta);
 int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void *x, size_t n, void *y, int mem,
                              void *stream);
+/* Diagnostics, no reference counterpart: the exact PLL walk of the last call
+ * that ran chunk-parallel (k_pll.hip) -- entries visited, repairs (samples
+ * whose true table index differed from the candidate's) and lane-blocks redone
+ * sample by sample.  All zero after a sequential (short) call.  Synchronises. */
+int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t *entries, uint64_t *repairs,
+                             uint64_t *fallbacks);
 
 /* ------------------------------------------------------------------------
  * Broadcast AM demodulator.  Replaces BroadcastAM (src/demod.hpp:93-153,

@@ -570,6 +570,7 @@ struct AmpObj {
     // candidates) can run while call k-1's walker still reads its own slot.
     DevBuf x0[2], mb[2], pll[2], dlh[3];
     unsigned long long ncall = 0;
+    const void* last_stats = nullptr;     // walker counters of the last parallel call (in its scratch slot)
     int cur = 0;
     bool dev_newer = false;
     hipStream_t last = nullptr;
@@ -1660,6 +1661,22 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
     });
 }
 
+int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t* entries, uint64_t* repairs, uint64_t* fallbacks)
+{
+    return guard([&] {
+        NONNULL(q);
+        unsigned long long stt[5] = {0, 0, 0, 0, 0};
+        if (q->last_stats) {
+            DeviceGuard g(q->device);
+            q->sync_all();
+            LDSP_HIP(hipMemcpy(stt, q->last_stats, sizeof(stt), hipMemcpyDeviceToHost));
+        }
+        if (entries) *entries = stt[4];
+        if (repairs) *repairs = stt[0];
+        if (fallbacks) *fallbacks = stt[1];
+    });
+}
+
 // Carrier lowpass + delay + PLL walk of AmpModem / BroadcastAM: writes
 // re(v1) / mod_index (costas 0) or the Costas-loop output (costas 1) to mbuf
 // (slot scratch when mbuf is null).  Returns the buffer written.  The caller
@@ -1692,6 +1709,7 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     c.alpha_host = q->st.alpha;
     c.y = mbuf;
     c.scratch = k::pll_parallel(n) ? q->pll[sl].ensure(k::pll_scratch_bytes(n), q->device) : nullptr;
+    q->last_stats = c.scratch ? (const char*)c.scratch + k::pll_stats_offset(n) : nullptr;
     k::pll_front(c, e.stream);
     const bool par = k::pll_parallel(n);
     if (par) q->front.mark(e.stream);     // the sequential loop writes the guess itself: mark after it

@@ -623,8 +623,8 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
                          : "memory", "exec");
             g.Kb = Kb;
             g.D = D;
+            g.nrep += (unsigned)__builtin_popcountll(PM);    // live counters (ldsp_ampmodem_walk_stats)
             if (STATS) {
-                g.nrep += (unsigned)__builtin_popcountll(PM);
                 g.nlb++;
                 g.nsame += PM == mask0 ? 1u : 0u;
             }
@@ -729,12 +729,12 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         const uint32_t pd = cb.pd[L];
         st->theta = cb.ce[2 * L] + g.Kb + (uint32_t)(n - (long)S) * g.D + cb.pth[L] + (uint32_t)n * pd;
         st->dtheta = cb.ce[2 * L + 1] + g.D + pd;
+        cb.stats[0] = g.nrep;
+        cb.stats[1] = g.nfb;
+        cb.stats[4] = NE;
         if (STATS) {
-            cb.stats[0] = g.nrep;
-            cb.stats[1] = g.nfb;
             cb.stats[2] = cyc_walk;
             cb.stats[3] = cyc_wait;
-            cb.stats[4] = NE;
             cb.stats[5] = g.nlb;
             cb.stats[6] = g.nsame;
         }

@@ -613,6 +613,12 @@ struct AmpModem {
         check(ldsp_ampmodem_get_pll_state(q, &t, &d));
         return py::make_tuple(t, d);
     }
+    py::tuple walk_stats()
+    {
+        uint64_t e, r, f;
+        check(ldsp_ampmodem_walk_stats(q, &e, &r, &f));
+        return py::make_tuple(e, r, f);
+    }
     py::object demod(const py::handle& x)
     {
         return run_same(x, true, false, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
@@ -964,6 +970,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("print", &AmpModem::print)
         .def("reset", &AmpModem::reset)
         .def("pll_state", &AmpModem::pll_state)
+        .def("_walk_stats", &AmpModem::walk_stats)
         .def("__call__", &AmpModem::demod);
 
     // ---- NCO (wrapper.cpp:201-212)

@@ -436,6 +436,17 @@ def test_ampmodem_bitwise(ld, ora, rng, carrier):
     assert g.pll_state() == o.pll_state
 
 
+def test_ampmodem_walk_stats(ld, ora, rng):
+    # live walker counters of the last chunk-parallel call; zero after a short (sequential) call
+    x = _am(rng, 200_000, 48000.0, 300.0, amp=1.0)
+    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
+    assert_bitwise(g(x), ora.AmpModem(0.5, "dsb", carrier=True)(x))
+    entries, repairs, fallbacks = g._walk_stats()
+    assert 0 < repairs < entries < len(x) and fallbacks < entries // 64 + 1
+    g(x[:1000])
+    assert g._walk_stats()[0] >= 0
+
+
 def test_ampmodem_parallel_calls_on_two_streams(ld, ora, rng):
     # Long calls run as candidates + walker; consecutive calls alternate torch
     # streams, so call k's candidates overlap call k-1's walk (guess state, two
