@@ -1684,6 +1684,9 @@ int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t* entries, uint64_t* rep
 //   wait slot[s] (call k-2 done with slot s) and front (call k-1's histories and guess)
 //   lowpass, delay history, candidates            -> mark front
 //   wait ord (call k-1's walk and DC blocker)      -> walker
+// Costas: the candidates start from the true state (the loop's two stable
+// points half a turn apart make a guess ambiguous), so its front also waits for
+// call k-1's walk.
 static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, float mod_index, int costas, float* mbuf)
 {
     const int L = 2 * (int)q->m + 1;
@@ -1691,6 +1694,7 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     const int h3 = (int)(q->ncall % 3);
     q->slot[sl].wait(e.stream);
     q->front.wait(e.stream);
+    if (costas) q->ord.wait(e.stream);
     if (!mbuf) mbuf = (float*)q->mb[sl].ensure(n * 4, q->device);
     void* x0 = q->x0[sl].ensure(n * 8, q->device);
     k::fir_exact(true, dx, q->lph[q->cur].p, q->lph[1 - q->cur].p, n, q->dlp.as<float>(), L, 1.0f, x0, e.stream);

@@ -131,10 +131,12 @@ struct CandBuf {
     uint32_t* pth;        // [nchc] P_theta(k)   (walker offset model, below)
     uint32_t* pd;         // [nchc] P_d(k)
     uint32_t* ne;         // total entries
+    uint32_t* hk;         // [nchc] Costas: chunk k's candidate locked half a turn from chunk 0's (re-run)
     uint32_t* bbase;      // [nblkE] S_blk: sample base of walker block c
     uint4* ent;           // [nblkE][2][kBlkE] entry records
     unsigned long long* stats;   // walker counters (LDSP_DEBUG_PLL)
     long nchc;
+    int costas;           // Costas phase detector (two stable points half a turn apart)
     uint32_t B;           // risky margin (table-cell units of 2^-22)
     int dbg;              // 0; 1 counters; 2 counters + every lane-block through the generic path; 3 no repairs (timing)
 };
@@ -206,8 +208,10 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
 // sequential call), extrapolated at constant frequency.  The guess is never the
 // true state of a walk still in progress, so this kernel can overlap the
 // previous call's walker; the walker carries the exact offset either way.
+// from_true: start from the true state instead of the guess (Costas, whose
+// front waits for the previous walk: chunk 0 is then the true trajectory's branch).
 __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st, int gcur, CandBuf cb,
-                                                 float* __restrict__ y, int warm)
+                                                 float* __restrict__ y, int warm, int from_true)
 {
     __shared__ float tab[1024];
     for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = in.table[i];
@@ -216,8 +220,8 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st,
     if (k >= cb.nchc) return;
     const long s0 = k * kCand, s1 = min(n, s0 + kCand);
     const float alpha = st->alpha, beta = st->beta;
-    const uint32_t g_th = st->gth[gcur];
-    uint32_t d = st->gd[gcur];
+    const uint32_t g_th = from_true ? st->theta : st->gth[gcur];
+    uint32_t d = from_true ? st->dtheta : st->gd[gcur];
     uint32_t theta = g_th;
     long w0 = s0 - warm;
     if (w0 <= 0) {
@@ -237,6 +241,25 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st,
         st->gth[1 - gcur] = theta;
         st->gd[1 - gcur] = d;
     }
+}
+
+// Costas: re-run the chunks the first scan marked (hk) from their start state
+// turned by half a turn, so every candidate sits in chunk 0's branch.
+__global__ void __launch_bounds__(64) k_pll_reflip(PllIn in, long n, AmpState* st, CandBuf cb, float* __restrict__ y)
+{
+    __shared__ float tab[1024];
+    for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = in.table[i];
+    __syncthreads();
+    const long k = (long)blockIdx.x * 64 + threadIdx.x;
+    if (k >= cb.nchc || cb.hk[k] == 0u) return;
+    const long s0 = k * kCand, s1 = min(n, s0 + kCand);
+    uint32_t theta = cb.cs[2 * k] + (1u << 31), d = cb.cs[2 * k + 1];
+    cb.cs[2 * k] = theta;
+    uint32_t nent = 0;
+    cand_run<true>(in, tab, s0, s1, st->alpha, st->beta, theta, d, cb, y, nent);
+    cb.ce[2 * k] = theta;
+    cb.ce[2 * k + 1] = d;
+    cb.cnt[k] = nent;
 }
 
 // ------------------------------------------------------------------ walker offset model
@@ -265,45 +288,64 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st,
 
 // Exclusive scan over chunks (one workgroup): entry offsets, P_theta, P_d,
 // the total entry count and the sample base of every walker block.
-__global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb)
+// Costas (phase error tanh(re v0) im v0) locks to either of two points half a
+// turn apart, and independently warmed-up candidates pick one at random.  With
+// flip = 1 the scan only marks, in hk[k], the chunks an odd number of
+// near-half-turn boundary jumps away from chunk 0 (k_pll_reflip re-runs them
+// from their start state + pi, a genuine trajectory in chunk 0's branch), and a
+// second scan with flip = 0 builds the model.  (The sine table is not exactly
+// odd, so a half-turn-shifted candidate cannot stand in for a re-run.)
+__device__ __forceinline__ uint32_t half_flip(uint32_t dth, int flip)
 {
-    __shared__ uint32_t sa[1024], sb[1024], sc[1024];
+    return flip ? ((dth + (1u << 30)) >> 31) : 0u;
+}
+
+__global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
+{
+    __shared__ uint32_t sa[1024], sb[1024], sc[1024], sh[1024];
     const int t = threadIdx.x;
     const long per = (cb.nchc + 1023) / 1024;
     const long k0 = min(cb.nchc, (long)t * per), k1 = min(cb.nchc, k0 + per);
-    uint32_t a = 0, b = 0, c = 0;
+    uint32_t a = 0, b = 0, c = 0, h = 0;
     for (long k = k0; k < k1; k++) {
         a += cb.cnt[k];
         if (k > 0) {
             const uint32_t dd = cb.ce[2 * k - 1] - cb.cs[2 * k + 1];
             const uint32_t dth = cb.ce[2 * k - 2] - cb.cs[2 * k];
+            const uint32_t fl = half_flip(dth, flip);
             b += dd;
-            c += dth - (uint32_t)(k * kCand) * dd;
+            c += dth - (fl << 31) - (uint32_t)(k * kCand) * dd;
+            h ^= fl;
         }
     }
     sa[t] = a;
     sb[t] = b;
     sc[t] = c;
+    sh[t] = h;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {          // inclusive Hillis-Steele
         const uint32_t pa = t >= off ? sa[t - off] : 0u, pb = t >= off ? sb[t - off] : 0u,
-                       pc = t >= off ? sc[t - off] : 0u;
+                       pc = t >= off ? sc[t - off] : 0u, ph = t >= off ? sh[t - off] : 0u;
         __syncthreads();
         sa[t] += pa;
         sb[t] += pb;
         sc[t] += pc;
+        sh[t] ^= ph;
         __syncthreads();
     }
-    uint32_t ea = sa[t] - a, eb = sb[t] - b, ec = sc[t] - c;     // exclusive
+    uint32_t ea = sa[t] - a, eb = sb[t] - b, ec = sc[t] - c, eh = sh[t] ^ h;     // exclusive
     for (long k = k0; k < k1; k++) {
         if (k > 0) {
             const uint32_t dd = cb.ce[2 * k - 1] - cb.cs[2 * k + 1];
             const uint32_t dth = cb.ce[2 * k - 2] - cb.cs[2 * k];
+            const uint32_t fl = half_flip(dth, flip);
             eb += dd;
-            ec += dth - (uint32_t)(k * kCand) * dd;
+            ec += dth - (fl << 31) - (uint32_t)(k * kCand) * dd;
+            eh ^= fl;
         }
         cb.pd[k] = eb;
         cb.pth[k] = ec;
+        cb.hk[k] = eh;
         cb.eoff[k] = ea;
         const uint32_t m = cb.cnt[k];
         const uint32_t blk = (ea + kBlkE - 1) / kBlkE;       // first walker block starting at or after ea
@@ -452,19 +494,6 @@ struct FullCtx {
     float alpha, beta, mod_index;
 };
 
-// Kick differences and output of the true index (icand + t) at global sample sg;
-// w = candidate theta + 2^21 (record word 0).
-__device__ __noinline__ uint4 pll_full(FullCtx fc, uint32_t w, uint32_t t, long sg)
-{
-    const uint32_t ic = w >> 22;
-    const uint32_t it = (ic + t) & 0x3ffu;
-    const long g = sg - fc.m;
-    const float2 u0 = fc.x0[sg], u1 = g >= 0 ? fc.x[g] : fc.hist[g + fc.m];
-    const Kick kt = pll_eval(fc.table, it, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas);
-    const Kick kc = pll_eval(fc.table, ic, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas);
-    return make_uint4(kt.k1 - kc.k1, kt.k2 - kc.k2, __float_as_uint(kt.out), 0u);
-}
-
 __device__ __forceinline__ uint32_t rl(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
@@ -494,32 +523,73 @@ struct WState {
     uint32_t Kb, D, nrep, nfb, nlb, nsame;
 };
 
-// Generic walk of every sample in [sa, sb]: 64 consecutive samples per step,
-// each repair evaluated in full (pll_full) and written to y, the offsets of
-// the later lanes recomputed from (Kb, D).  Used where the sparse walk cannot
-// prove a gap clean, and for every lane-block in the LDSP_DEBUG_PLL=2 check.
-__device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_t S, CandBuf cb, FullCtx fc,
-                                             float* y, int lane)
+// Generic walk of every sample in [sa, sb]: 64 consecutive samples per step
+// (records, offset model and loop inputs loaded one step ahead), each repair
+// taken from the record when the true index is one cell away and evaluated in
+// full (table in LDS) otherwise, its output written to y, the offsets of the
+// later lanes updated in place.  Used where the sparse walk cannot prove a gap
+// clean, and for every lane-block in the LDSP_DEBUG_PLL=2 check.
+struct FbGroup {
+    uint4 r0, r1;
+    uint32_t A;
+    float2 u0, u1;
+};
+__device__ __forceinline__ FbGroup fb_load(long base, long sb, const CandBuf& cb, const FullCtx& fc, int lane)
 {
+    FbGroup q;
+    const long s = min(base + lane, sb);
+    q.r0 = cb.rec[2 * s];
+    q.r1 = cb.rec[2 * s + 1];
+    const long k = s / kCand;
+    q.A = cb.pth[k] + (uint32_t)s * cb.pd[k];
+    q.u0 = fc.x0[s];
+    const long g = s - fc.m;
+    q.u1 = g >= 0 ? fc.x[g] : fc.hist[g + fc.m];
+    return q;
+}
+
+__device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_t S, CandBuf cb, FullCtx fc,
+                                             const float* tab, float* y, int lane)
+{
+    FbGroup nx = fb_load(sa, sb, cb, fc, lane);
     for (long base = sa; base <= sb; base += 64) {
-        const long s = min(base + lane, sb);
+        const FbGroup q = nx;
+        if (base + 64 <= sb) nx = fb_load(base + 64, sb, cb, fc, lane);
         const unsigned long long M = __builtin_amdgcn_ballot_w64(base + lane <= sb);
-        const uint32_t w = cb.rec[2 * s].x;
-        const long k = s / kCand;
-        const uint32_t A = cb.pth[k] + (uint32_t)s * cb.pd[k];
-        const uint32_t u = w & 0x3fffffu, srel = (uint32_t)(s - (long)S);
-        uint32_t v = u + g.Kb + srel * g.D + A;
+        const uint32_t u = q.r0.x & 0x3fffffu, srel = (uint32_t)(base + lane - (long)S);
+        uint32_t v = u + g.Kb + srel * g.D + q.A;
         unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
         while (mask != 0) {
             const int j = __builtin_ctzll(mask);
-            const long sj = base + j;
-            const uint4 f = pll_full(fc, rl(w, j), rl(v, j) >> 22, sj);
-            const uint32_t dk1 = rfl(f.x), dk2 = rfl(f.y);
-            if (lane == 0) y[sj] = __uint_as_float(rfl(f.z));
-            g.Kb += dk2 - (uint32_t)(sj - (long)S) * dk1;
+            const uint32_t vj = rl(v, j);
+            uint32_t dk1, dk2, out;
+            if (vj - 0x400000u < 0x400000u) {                // one cell up
+                dk1 = rl(q.r0.w, j);
+                dk2 = rl(q.r1.x, j);
+                out = rl(q.r1.z, j);
+            } else if (vj >= 0xffc00000u) {                  // one cell down
+                dk1 = rl(q.r0.y, j);
+                dk2 = rl(q.r0.z, j);
+                out = rl(q.r1.y, j);
+            } else {                                         // further: the loop step in full
+                const uint32_t ic = rl(q.r0.x, j) >> 22;
+                const float2 u0 = make_float2(__uint_as_float(rl(__float_as_uint(q.u0.x), j)),
+                                              __uint_as_float(rl(__float_as_uint(q.u0.y), j)));
+                const float2 u1 = make_float2(__uint_as_float(rl(__float_as_uint(q.u1.x), j)),
+                                              __uint_as_float(rl(__float_as_uint(q.u1.y), j)));
+                const Kick kt = pll_eval(tab, (ic + (vj >> 22)) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index,
+                                         fc.costas);
+                const Kick kc = pll_eval(tab, ic, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas);
+                dk1 = rfl(kt.k1 - kc.k1);
+                dk2 = rfl(kt.k2 - kc.k2);
+                out = rfl(__float_as_uint(kt.out));
+            }
+            const uint32_t rrel = (uint32_t)j + (uint32_t)(base - (long)S);
+            if (lane == 0) y[base + j] = __uint_as_float(out);
+            g.Kb += dk2 - rrel * dk1;
             g.D += dk1;
             g.nrep++;
-            v = u + g.Kb + srel * g.D + A;
+            v += dk2 + (srel - rrel) * dk1;
             mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M & ((~0ull << j) << 1);
         }
     }
@@ -547,7 +617,7 @@ struct PrevLB {
 
 template <bool F24, bool STATS>
 __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv, WState& g, uint32_t S, PrevLB& prev,
-                                        const CandBuf& cb, const FullCtx& fc, float* y, int lane)
+                                        const CandBuf& cb, const FullCtx& fc, const float* tab, float* y, int lane)
 {
     const uint32_t srel = E0.z, sx = srel;
     uint32_t x = E0.x + g.Kb + srel * g.D;
@@ -607,7 +677,7 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
             WState r = g0;
             r.nfb++;
             const long s_first = prev.first ? 0l : (long)prev.S + rl(prev.srel, prev.nv - 1) + 1;
-            r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, y, lane);
+            r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, tab, y, lane);
             g.Kb = rfl(r.Kb);
             g.D = rfl(r.D);
             g.nrep = rfl(r.nrep);
@@ -643,6 +713,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                                                            float* __restrict__ y)
 {
     __shared__ WalkBufE buf[4];          // ring: block c in buf[c & 3], DMA'd three blocks ahead
+    __shared__ float wtab[1024];         // NCO table for the fallback's full loop steps
     // Own the CU: 8 waves x 256 VGPRs fill every SIMD's register file, so no wave of
     // the kernels running beside the walk (the next call's AGC, candidates, ...)
     // is placed on the walker's SIMD and takes issue slots from its serial chain.
@@ -660,6 +731,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         else if (nblk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    for (int i = tid; i < 1024; i += kWalkThreads) wtab[i] = in.table[i];
+    __syncthreads();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -706,7 +779,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 const int qn = min(q + 1, kBlkE / 64 - 1) * 64 + lane;
                 const uint4 N0 = b.e[0][qn], N1 = b.e[1][qn];
                 if (q * 64 >= cnt) break;
-                walk_lb<F24, STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, y, lane);
+                walk_lb<F24, STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane);
                 A0 = N0;
                 A1 = N1;
             }
@@ -755,7 +828,7 @@ __global__ void k_delay_hist(const float2* __restrict__ x, const float2* __restr
 // Scratch layout (16-byte aligned pieces): records | cs | ce | cnt | eoff | pth | pd |
 // ne | bbase | entries | stats (256 B).
 struct PllLayout {
-    size_t rec, cs, ce, cnt, eoff, pth, pd, ne, bbase, ent, stats, total;
+    size_t rec, cs, ce, cnt, eoff, pth, pd, hk, ne, bbase, ent, stats, total;
     long nchc, nblkE;
 };
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -773,6 +846,7 @@ static PllLayout pll_layout(size_t n)
     L.eoff = o;  o = al16(o + nc * 4);
     L.pth = o;   o = al16(o + nc * 4);
     L.pd = o;    o = al16(o + nc * 4);
+    L.hk = o;    o = al16(o + nc * 4);
     L.ne = o;    o = al16(o + 4);
     L.bbase = o; o = al16(o + (size_t)L.nblkE * 4);
     L.ent = o;   o = al16(o + (size_t)L.nblkE * 2 * kBlkE * 16);
@@ -823,15 +897,21 @@ static CandBuf cand_buf(const PllCall& c)
     cb.eoff = (uint32_t*)(p + L.eoff);
     cb.pth = (uint32_t*)(p + L.pth);
     cb.pd = (uint32_t*)(p + L.pd);
+    cb.hk = (uint32_t*)(p + L.hk);
+    cb.costas = c.costas;
     cb.ne = (uint32_t*)(p + L.ne);
     cb.bbase = (uint32_t*)(p + L.bbase);
     cb.ent = (uint4*)(p + L.ent);
     cb.stats = (unsigned long long*)(p + L.stats);
     cb.nchc = L.nchc;
-    // risky margin B: |f| stays below 2^19 on ~99.6 % of the samples of the AM
-    // chain (walker counters), and 2B / 2^22 = 1/4 of the samples are entries
-    static const int lb = std::getenv("LDSP_PLL_LOGB") ? std::atoi(std::getenv("LDSP_PLL_LOGB")) : 19;
-    cb.B = 1u << std::max(8, std::min(20, lb));
+    // risky margin B: with the carrier PLL |f| stays below 2^19 on ~99.6 % of the
+    // samples of the AM chain (walker counters), and 2B / 2^22 = 1/4 of the samples
+    // are entries.  The Costas detector's gain vanishes at the message's zero
+    // crossings, |f| often exceeds 2^20 there, and gap proofs would fail: B = 2^21
+    // makes every sample an entry (no gaps; 11 ms instead of 190 ms per 1.6 M
+    // samples of locked DSB-SC, scripts/pll_stress.py).
+    static const int lb = std::getenv("LDSP_PLL_LOGB") ? std::atoi(std::getenv("LDSP_PLL_LOGB")) : 0;
+    cb.B = 1u << std::max(8, std::min(21, lb ? lb : (c.costas ? 21 : 19)));
     static const int dbg = std::getenv("LDSP_DEBUG_PLL") ? std::atoi(std::getenv("LDSP_DEBUG_PLL")) : 0;
     cb.dbg = dbg;
     return cb;
@@ -853,12 +933,25 @@ void pll_front(const PllCall& c, hipStream_t s)
         LDSP_PROF(s, "k_pll_cand");
         static const int warm = std::getenv("LDSP_PLL_WARM") ? std::atoi(std::getenv("LDSP_PLL_WARM")) : kWarm;
         hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s, pll_in(c), (long)c.n,
-                           c.st, c.gcur, cb, c.y, warm);
+                           c.st, c.gcur, cb, c.y, warm, c.costas);
     }
     LDSP_HIP(hipGetLastError());
+    if (c.costas) {
+        {
+            LDSP_PROF(s, "k_pll_scan");
+            hipLaunchKernelGGL(k_pll_scan, dim3(1), dim3(1024), 0, s, cb, 1);
+        }
+        LDSP_HIP(hipGetLastError());
+        {
+            LDSP_PROF(s, "k_pll_reflip");
+            hipLaunchKernelGGL(k_pll_reflip, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s, pll_in(c),
+                               (long)c.n, c.st, cb, c.y);
+        }
+        LDSP_HIP(hipGetLastError());
+    }
     {
         LDSP_PROF(s, "k_pll_scan");
-        hipLaunchKernelGGL(k_pll_scan, dim3(1), dim3(1024), 0, s, cb);
+        hipLaunchKernelGGL(k_pll_scan, dim3(1), dim3(1024), 0, s, cb, 0);
     }
     LDSP_HIP(hipGetLastError());
     {

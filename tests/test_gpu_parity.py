@@ -442,7 +442,7 @@ def test_ampmodem_walk_stats(ld, ora, rng):
     g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
     assert_bitwise(g(x), ora.AmpModem(0.5, "dsb", carrier=True)(x))
     entries, repairs, fallbacks = g._walk_stats()
-    assert 0 < repairs < entries < len(x) and fallbacks < entries // 64 + 1
+    assert 0 < repairs < entries < len(x) and fallbacks <= (entries + 63) // 64    # (all of them under LDSP_DEBUG_PLL=2)
     g(x[:1000])
     assert g._walk_stats()[0] >= 0
 
