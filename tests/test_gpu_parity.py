@@ -447,15 +447,24 @@ def test_ampmodem_walk_stats(ld, ora, rng):
     assert g._walk_stats()[0] >= 0
 
 
-def test_ampmodem_parallel_calls_on_two_streams(ld, ora, rng):
+@pytest.mark.parametrize("carrier", [True, False])
+def test_ampmodem_parallel_calls_on_two_streams(ld, ora, rng, carrier):
     # Long calls run as candidates + walker; consecutive calls alternate torch
     # streams, so call k's candidates overlap call k-1's walk (guess state, two
     # scratch slots, three history buffers).  Short calls interleave the
     # sequential loop.  Everything must stay bit-identical to one sequential run.
     import torch
-    x = _am(rng, 6 * 20_000 + 3000, 48000.0, 300.0, amp=1.0)
-    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
-    o = ora.AmpModem(0.5, "dsb", carrier=True)
+    # (carrier=False: a DSB-SC signal for the Costas loop, whose candidates start
+    # from the true state and whose half-turn-flipped chunks are re-run)
+    if carrier:
+        x = _am(rng, 6 * 20_000 + 3000, 48000.0, 300.0, amp=1.0)
+    else:
+        n = 6 * 20_000 + 3000
+        t = np.arange(n) / 48000.0
+        m = (np.sin(2 * np.pi * 400 * t) + np.sin(2 * np.pi * 1000 * t)) / 2
+        x = (m * np.exp(1j * (2 * np.pi * 100 * t + 0.7)) + 0.02 * cgauss(rng, n)).astype(np.complex64)
+    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=carrier)
+    o = ora.AmpModem(0.5, "dsb", carrier=carrier)
     xd = torch.from_numpy(x).cuda()
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     torch.cuda.synchronize()
