@@ -641,17 +641,22 @@ __device__ __forceinline__ void mv_acc(const double* __restrict__ M, const doubl
     }
 }
 
+// The staging tiles and the scan buffer share LDS (they are used in separate
+// phases, fenced by __syncthreads): 35 KB per block, and at most 168 VGPRs, so
+// three blocks (12 waves) fit a CU to hide the HBM latency of the tile stream.
 template <int NC, int D, bool FINAL, class Step>
-__global__ void __launch_bounds__(kBN) k_iir_blk(Step step, const float* __restrict__ xf, long n, long nch,
-                                                 const double* __restrict__ AL, double* __restrict__ Lloc,
-                                                 const double* __restrict__ BS, double* __restrict__ BL,
-                                                 double* __restrict__ state64, float* __restrict__ yf)
+__global__ void __launch_bounds__(kBN) __attribute__((amdgpu_waves_per_eu(3)))
+k_iir_blk(Step step, const float* __restrict__ xf, long n, long nch, const double* __restrict__ AL,
+          double* __restrict__ Lloc, const double* __restrict__ BS, double* __restrict__ BL,
+          double* __restrict__ state64, float* __restrict__ yf)
 {
     using S = SampT<NC>;
     using T = typename S::T;
     constexpr int kRow = kBT + 1;
-    __shared__ T stage[kBN / 64][64 * kRow];
-    __shared__ double scn[kBN][NC][D];
+    constexpr size_t kStage = sizeof(T) * (kBN / 64) * 64 * kRow, kScn = sizeof(double) * kBN * NC * D;
+    __shared__ __attribute__((aligned(16))) char lds[kStage > kScn ? kStage : kScn];
+    T (*stage)[64 * kRow] = reinterpret_cast<T (*)[64 * kRow]>(lds);
+    double (*scn)[NC][D] = reinterpret_cast<double (*)[NC][D]>(lds);
     const T* __restrict__ x = (const T*)xf;
     T* __restrict__ y = (T*)yf;
     const int t = threadIdx.x;
@@ -759,6 +764,7 @@ __global__ void __launch_bounds__(kBN) k_iir_blk(Step step, const float* __restr
         }
     }
     // inclusive scan over the block's chunks: E_j = L_j + A^C E_{j-1}
+    __syncthreads();                     // every wave done with the staging tiles (same LDS)
 #pragma unroll
     for (int c = 0; c < NC; c++)
 #pragma unroll
@@ -796,6 +802,7 @@ __global__ void __launch_bounds__(kBN) k_iir_blk(Step step, const float* __restr
     for (int c = 0; c < NC; c++)
 #pragma unroll
         for (int i = 0; i < D; i++) v[c][i] = t == 0 ? BS[(b * NC + c) * D + i] : scn[t - 1][c][i];
+    __syncthreads();                     // scan buffer read: the staging tiles may reuse it
     run(std::true_type{});
     if (gc == nch - 1)
 #pragma unroll
