@@ -455,6 +455,27 @@ def host_path(L, device, n=16 << 20, reps=3):
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / reps
         res[name] = {"ms": round(el * 1e3, 2), "Msamples_s": round(n / el / 1e6, 1)}
+    # the README's SDR callback block: 65 536 IQ samples per numpy call (the
+    # reference's own loop), and the same blocks as device tensors
+    blk, nblk = 65536, 64
+    for name, mk in (("readme_65536_numpy", lambda i: xh[i * blk:(i + 1) * blk]),
+                     ("readme_65536_device", lambda i, xd=torch.from_numpy(xh[:blk * nblk]).to(device):
+                      xd[i * blk:(i + 1) * blk])):
+        for nst in ((1,) if name.endswith("numpy") else (1, 3)):
+            radio = AMRadio(L)
+            strm = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(nst - 1)]
+            for i in range(4):
+                with torch.cuda.stream(strm[i % nst]):
+                    radio(mk(i))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(nblk):
+                with torch.cuda.stream(strm[i % nst]):
+                    radio(mk(i))
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            res[name + ("" if nst == 1 else f"_{nst}streams")] = {"ms_per_block": round(el / nblk * 1e3, 3),
+                                                                  "Msamples_s": round(blk * nblk / el / 1e6, 1)}
     return res
 
 

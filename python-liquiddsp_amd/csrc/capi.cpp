@@ -1546,7 +1546,10 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             q->hist[1].ensure((size_t)hl * 8, q->device);
         }
         const bool spec = !nospec && q->hist_valid >= hl;
-        const bool par = n >= (size_t)4 * (W + Wa);
+        // chunk-parallel once it beats the one-lane loop: its latency is Wa approximate + W + 256
+        // exact steps (~1.6 ms at bandwidth 0.01) against ~0.57 us per sample sequentially
+        static const size_t parmin = std::getenv("LDSP_AGC_PARMIN") ? (size_t)std::atol(std::getenv("LDSP_AGC_PARMIN")) : 0;
+        const bool par = n >= (parmin ? parmin : (size_t)(0.7 * (0.16 * Wa + 0.43 * (W + 256)) / 0.57) + 256);
         k::SpecPlan p;
         if (n > 0 && par) {
             p.W = W;

@@ -830,7 +830,11 @@ void launch_blk(const Step& st, const IirDesc& d, const float* x, size_t n, doub
     cp.AG = p.AG;
     cp.local = p.blocal;
     cp.carry = p.bstart;
-    launch_carry<D>(NC, cp, state64, s);
+    if (p.nblk == 1) {                  // one block: its start state is the call's
+        LDSP_HIP(hipMemcpyAsync(p.bstart, state64, sizeof(double) * NC * D, hipMemcpyDeviceToDevice, s));
+    } else {
+        launch_carry<D>(NC, cp, state64, s);
+    }
     {
         LDSP_PROF(s, "k_iir_blk_final");
         hipLaunchKernelGGL((k_iir_blk<NC, D, true, Step>), dim3(g), dim3(kBN), 0, s, st, x, (long)n, p.nchunks,

@@ -870,7 +870,11 @@ void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m
     LDSP_HIP(hipGetLastError());
 }
 
-bool pll_parallel(size_t n) { return n >= (size_t)4 * kWarm; }
+// Candidates + walk beat the one-lane loop (~0.57 us per sample) from about two
+// thousand samples: their latency is the warm-up plus one recorded chunk
+// (~0.94 ms), then the walk.
+static const size_t kParMin = std::getenv("LDSP_PLL_PARMIN") ? (size_t)std::atol(std::getenv("LDSP_PLL_PARMIN")) : 2048;
+bool pll_parallel(size_t n) { return n >= kParMin; }
 
 static PllIn pll_in(const PllCall& c)
 {
