@@ -160,17 +160,28 @@ __device__ __forceinline__ void agc_run(AgcReg& r, const AgcState& p, const X& x
     }
 }
 
-__global__ void k_agc_seq(const float2* __restrict__ x, long n, AgcState* st, float2* __restrict__ y,
-                          uint8_t* __restrict__ status)
+// One lane runs the loop; the wave stages the input through LDS 2048 samples
+// at a time so the loop never waits on a global load.
+__global__ void __launch_bounds__(64) k_agc_seq(const float2* __restrict__ x, long n, AgcState* st,
+                                                float2* __restrict__ y, uint8_t* __restrict__ status)
 {
-    if (threadIdx.x != 0) return;
+    constexpr int kS = 2048;
+    __shared__ float2 xs[kS];
     const AgcState p = *st;
     AgcReg r{p.g, p.y2p, p.mode, p.timer};
-    agc_run<true>(r, p, x, 0, n, y, status);
-    st->g = r.g;
-    st->y2p = r.y2p;
-    st->mode = r.mode;
-    st->timer = r.timer;
+    for (long base = 0; base < n; base += kS) {
+        const int cnt = (int)min((long)kS, n - base);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += 64) xs[i] = x[base + i];
+        __syncthreads();
+        if (threadIdx.x == 0) agc_run<true>(r, p, (const float2*)xs, 0, cnt, y + base, status ? status + base : nullptr);
+    }
+    if (threadIdx.x == 0) {
+        st->g = r.g;
+        st->y2p = r.y2p;
+        st->mode = r.mode;
+        st->timer = r.timer;
+    }
 }
 
 // scratch: [nchunks][2 (start, end)][4 words: g, y2p, mode, timer]

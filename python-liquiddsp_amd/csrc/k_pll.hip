@@ -82,6 +82,7 @@ __device__ __forceinline__ Kick pll_eval(const float* tab, uint32_t i, float2 u0
 // ------------------------------------------------------------------ sequential
 constexpr int kSeqChunk = 2048;
 
+template <bool COSTAS>
 __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st, int gcur, float* __restrict__ y)
 {
     __shared__ float tab[1024];
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
         __syncthreads();
         if (tid == 0) {
             for (int i = 0; i < cnt; i++) {
-                const Kick k = pll_eval(tab, tidx(theta), b0[i], b1[i], alpha, beta, in.mod_index, in.costas);
+                const Kick k = pll_eval(tab, tidx(theta), b0[i], b1[i], alpha, beta, in.mod_index, COSTAS ? 1 : 0);
                 d += k.k1;
                 theta += k.k2 + d;
                 y[base + i] = k.out;
@@ -971,7 +972,8 @@ void pll_back(const PllCall& c, hipStream_t s)
     if (!pll_parallel(c.n)) {
         {
             LDSP_PROF(s, "k_pll_seq");
-            hipLaunchKernelGGL(k_pll_seq, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
+            if (c.costas) hipLaunchKernelGGL(k_pll_seq<true>, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
+            else hipLaunchKernelGGL(k_pll_seq<false>, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
         }
         LDSP_HIP(hipGetLastError());
         return;
