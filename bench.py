@@ -154,6 +154,21 @@ def gather_pcm(y):
     return outs
 
 
+def host_info():
+    """the box's host CPU next to the CPU baseline (nproc, model, clock)."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name") and "model" not in info:
+                    info["model"] = line.split(":", 1)[1].strip()
+                elif line.startswith("cpu MHz") and "mhz" not in info:
+                    info["mhz"] = float(line.split(":", 1)[1])
+    except OSError:
+        pass
+    return info
+
+
 def cpu_baseline(n_iq, seconds=10.0):
     """Time the CPU restatement (oracle/, -O3, single thread) on a bounded sample."""
     from oracle import oracle as O
@@ -191,6 +206,8 @@ def main():
                     help="HIP streams the steps rotate over (1 = every step on torch's current stream). "
                          "Each object orders its own calls across streams (libldsp StreamMark), so step k+1's "
                          "IIR/resampler/AGC/candidate kernels overlap step k's serial PLL walk")
+    ap.add_argument("--channel", type=int, default=None,
+                    help="synthetic channel (carrier offset / seed) this rank demodulates; default: its rank")
     ap.add_argument("--no-kprof", action="store_true",
                     help="no per-kernel HIP events inside the timed steps (kernel times then come from a separate "
                          "profiled pass)")
@@ -212,7 +229,7 @@ def main():
     torch.cuda.set_device(device)
 
     import liquiddsp as L
-    x = synth_channel(args.n, rank, device)
+    x = synth_channel(args.n, rank if args.channel is None else args.channel, device)
     x_all = None
     if args.scatter and dist and rank == 0:
         x_all = torch.stack([x] + [synth_channel(args.n, r, device) for r in range(1, world)])
@@ -304,6 +321,8 @@ def main():
                                "-> de-emphasis), one independent channel per GPU",
                    "samples_per_step_per_gpu": args.n, "iq_rate": 2000000, "pcm_rate": 48000,
                    "pcm_samples_per_step": n_pcm,
+                   "carrier_hz": CARRIERS[(rank if args.channel is None else args.channel) % len(CARRIERS)],
+                   "seed": 4 if (rank if args.channel is None else args.channel) == 0 else 10 + (rank if args.channel is None else args.channel),
                    "parallelism": f"channel-per-gpu x{world}" + (" rank0-scatter/gather" if args.scatter and dist else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "ms_per_launch": round(dom_ms, 4),
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -327,6 +346,7 @@ def main():
         res["components"] = components(L, device)
     if rank == 0 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.n, args.cpu_seconds)
+        res["cpu_baseline"]["host"] = host_info()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist:
@@ -397,7 +417,28 @@ def components(L, device, reps=5):
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(16 * n / ms / 1e6 / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic("fir", "k_fir_fft512"), "traffic_source": PMC_SOURCE,
                 "alg_bytes": 16 * n, "target_frac": 0.5}
-    del xs
+    # BASELINE config 2: ComplexResampler(rate = 48 k / 2 M) on 64 Mi samples, as one
+    # call and as the README's 65 536-sample blocks (device tensors, one stream)
+    rs = L.ComplexResampler(rate=48000 / 2000000, Fc=48000 / 2000000)
+    t = timed(lambda: rs(xs))
+    nout = int(rs(xs[:65536]).numel())
+    rb = L.ComplexResampler(rate=48000 / 2000000, Fc=48000 / 2000000)
+    blocks = [xs[i:i + 65536] for i in range(0, 1 << 22, 65536)]
+    for b in blocks[:4]:
+        rb(b)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in blocks:
+        rb(b)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kr = [k for k in t if k.startswith("k_resamp")][0]
+    ab = 8 * n + 8 * round(n * 0.024)
+    out["resampler_64Mi"] = {"kernel": kr, "ms": round(t[kr], 4), "Msamples_s": round(n / t[kr] / 1e3, 1),
+                             "alg_GBs": round(ab / t[kr] / 1e6, 1), "hbm_frac": round(ab / t[kr] / 1e6 / HBM_PEAK_GBS, 4),
+                             "blocks_65536_Msamples_s": round(len(blocks) * 65536 / el / 1e6, 1),
+                             "outputs_per_65536": nout}
+    del xs, blocks
     n = 256 << 20
     xs = torch.complex(torch.randn(n, generator=g, device=device), torch.randn(n, generator=g, device=device))
     nco = L.NCO("nco")

@@ -1,4 +1,5 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "agc or ampmodem or amradio or broadcast or smoke" > gpurun_out/pt.log 2>&1 || { tail -20 gpurun_out/pt.log; exit 1; }
-tail -1 gpurun_out/pt.log
-BLK=65536 timeout -k 10 200 python scripts/readme_blocks.py 2>&1 | tail -1
+timeout -k 10 400 python bench.py --cpu-seconds 2 > gpurun_out/b.log 2>&1 || { tail -5 gpurun_out/b.log; exit 1; }
+python -c "
+import json; r=json.loads([l for l in open('gpurun_out/b.log') if l.startswith('{')][-1])
+print(r['value'], r['config']); print(r['components']['resampler_64Mi']); print(r['cpu_baseline'])"
