@@ -17,11 +17,11 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 # HIP hardware queues per process (read at HIP init, before torch loads it): the
-# chain rotates 3 streams and the multi-channel component 2 per channel; with
+# chain rotates 4 streams and the multi-channel component 2 per channel (16); with
 # HIP's default of 4 (also the GPU box's setting) those streams share queues and
 # serialise.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 32:
+    os.environ["GPU_MAX_HW_QUEUES"] = "32"
 for p in (REPO, os.path.join(REPO, "python-liquiddsp_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
@@ -456,24 +456,24 @@ def components(L, device, reps=5):
     return out
 
 
-def multi_channel(L, device, channels=8, steps=10, n=64 << 20):
+def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2):
     """SURVEY 8(e)'s caveat: independent channels also share one GPU -- each
     channel's serial PLL walk / AGC repair occupy one CU, so C channels on C
     stream pairs overlap.  Aggregate IQ Msamples/s of `channels` AMRadio chains
     (BASELINE config 4 each, carriers as the ranks of config 5) on this GPU."""
     xs = [synth_channel(n, r, device) for r in range(channels)]
     radios = [AMRadio(L) for _ in range(channels)]
-    strm = [[torch.cuda.Stream(device) for _ in range(2)] for _ in range(channels)]
+    strm = [[torch.cuda.Stream(device) for _ in range(per)] for _ in range(channels)]
 
     def step(k, w=None):
         kk = k if k is not None else w
         for c in range(channels):
-            with torch.cuda.stream(strm[c][kk % 2]):
+            with torch.cuda.stream(strm[c][kk % per]):
                 radios[c](xs[c])
 
     t = timed_steps(step, steps, 2, torch.cuda.synchronize, lambda: None)
     del xs
-    return {"channels": channels, "steps": steps, "ms_per_step": round(t / steps * 1e3, 3),
+    return {"channels": channels, "streams_per_channel": per, "steps": steps, "ms_per_step": round(t / steps * 1e3, 3),
             "Msamples_s": round(channels * n * steps / t / 1e6, 1),
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")}
 
