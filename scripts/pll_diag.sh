@@ -1,5 +1,6 @@
 #!/bin/bash
-# Walker diagnostics: counters (LDSP_DEBUG_PLL=1), skip-repair timing (=2),
+# Walker diagnostics: counters (LDSP_DEBUG_PLL=1), every lane-block through the
+# generic path (=2, exact, slow),
 # and the bench at 1..4 rotating streams (no components, no CPU baseline).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
