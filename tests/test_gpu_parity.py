@@ -386,6 +386,9 @@ def test_agc_speculative_calls_on_two_streams(ld, ora, rng):
             torch.cuda.synchronize()
             g.reset()
             o.reset()
+        if i == 4:                       # new bandwidth: new warm-up lengths, the history restarts
+            g.bandwidth = 0.02
+            o.bandwidth = np.float32(0.02)
         with torch.cuda.stream(streams[i % 2]):
             outs.append(g(xd[a:b]))
         refs.append(o(x[a:b]))
