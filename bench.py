@@ -196,7 +196,7 @@ def cpu_baseline(n_iq, seconds=10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
