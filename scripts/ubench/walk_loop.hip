@@ -74,6 +74,15 @@ __global__ void __launch_bounds__(64) k_loop(const uint4* E, uint32_t* out, int 
                 x = x + sx * dd.x + dd.y;
                 mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
             } while (mask != 0);
+        } else if (V == 6) {     // ds_bpermute broadcast of lane j's values into VGPRs
+            do {
+                const int j = __builtin_ctzll(mask);
+                const int a = j << 2;
+                const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)d1);
+                const uint32_t b2 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)d2);
+                x = x + sx * b1 + b2;
+                mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
+            } while (mask != 0);
         } else if (V == 3) {     // pure SALU loop over the mask (no ballot per step)
             do {
                 const int j = __builtin_ctzll(mask);
@@ -114,6 +123,7 @@ int main()
     run(k_loop<3>, "V3 no ballot (SALU mask walk)");
     run(k_loop<4>, "V4 readlane + s_mov");
     run(k_loop<5>, "V5 LDS broadcast");
+    run(k_loop<6>, "V6 ds_bpermute broadcast");
     // s_memtime frequency: compare against wall clock
     hipEvent_t a, b;
     hipEventCreate(&a);
