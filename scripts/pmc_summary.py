@@ -53,6 +53,10 @@ def main(root):
                 e["fetch_bytes_corrected"] = 2.0 * fe[k] * 1024
             if k in wr:
                 e["write_bytes"] = wr[k] * 1024
+            for cn in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM"):
+                sq = counters(os.path.join(root, f"{run}_sq"), cn)
+                if k in sq:
+                    e[cn.lower()] = round(sq[k])
             if "fetch_bytes_corrected" in e and "write_bytes" in e:
                 e["hbm_bytes"] = e["fetch_bytes_corrected"] + e["write_bytes"]
                 e["hbm_GBs"] = round(e["hbm_bytes"] / (e["avg_us"] * 1e3), 1)

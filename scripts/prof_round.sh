@@ -20,6 +20,7 @@ run bench_trace --kernel-trace --stats --output-format csv -d $out/bench_trace -
 run fir_trace --kernel-trace --stats --output-format csv -d $out/fir_trace -o fir -- $F
 run bench_fetch --pmc FETCH_SIZE --output-format csv -d $out/bench_fetch -o bench -- $B
 run bench_write --pmc WRITE_SIZE --output-format csv -d $out/bench_write -o bench -- $B
+run bench_sq --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM --output-format csv -d $out/bench_sq -o bench -- $B
 run fir_fetch --pmc FETCH_SIZE --output-format csv -d $out/fir_fetch -o fir -- $F
 run fir_write --pmc WRITE_SIZE --output-format csv -d $out/fir_write -o fir -- $F
 python3 scripts/pmc_summary.py $out > $out/summary.json && cat $out/summary.json
