@@ -344,7 +344,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_components:
         res["components"] = components(L, device)
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:      # the CPU leg runs at N = 1 only
         res["cpu_baseline"] = cpu_baseline(args.n, args.cpu_seconds)
         res["cpu_baseline"]["host"] = host_info()
     if rank == 0:
