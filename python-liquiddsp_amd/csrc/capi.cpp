@@ -509,9 +509,11 @@ struct AgcObj {
     int device = -1;
     DevBuf dst, status;
     // Per-call scratch in two slots (call parity) and the input history the
-    // speculative warm-ups read (the last hist_len samples before the call,
-    // ping-ponged: call k reads hist[k & 1] and writes hist[(k + 1) & 1]).
-    DevBuf scr[2], hist[2];
+    // speculative warm-ups read (the last hist_len samples before the call, in
+    // a ring of three: call k reads hist[k % 3] and writes hist[(k + 1) % 3], so
+    // call k + 1's front may start while call k's chunks still read theirs;
+    // call k + 2, which overwrites it, first waits for call k's back half).
+    DevBuf scr[2], hist[3];
     long hist_len = 0, hist_valid = 0;
     uint64_t ncall = 0;
     bool dev_newer = false;           // device state advanced past the mirror
@@ -1516,7 +1518,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         q->ensure_device();
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream);
-        const int sl = (int)(q->ncall & 1);
+        const int sl = (int)(q->ncall & 1), h3 = (int)(q->ncall % 3);
         q->slot[sl].wait(e.stream);
         q->front.wait(e.stream);
         if (q->upload_pending) {
@@ -1542,8 +1544,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         if (hl != q->hist_len) {             // bandwidth changed: history restarts
             q->hist_len = hl;
             q->hist_valid = 0;
-            q->hist[0].ensure((size_t)hl * 8, q->device);
-            q->hist[1].ensure((size_t)hl * 8, q->device);
+            for (int i = 0; i < 3; i++) q->hist[i].ensure((size_t)hl * 8, q->device);
         }
         const bool spec = !nospec && q->hist_valid >= hl;
         // chunk-parallel once it beats the one-lane loop: its latency is Wa approximate + W + 256
@@ -1558,13 +1559,16 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             p.C = 256;
             p.nchunks = (long)((n + p.C - 1) / p.C);
             p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks), q->device);
-            p.hist = q->hist[sl].p;
+            p.hist = q->hist[h3].p;
             p.H = spec ? (int)hl : 0;
+        }
+        // the next call's history first: its front then waits for this copy only
+        if (n > 0) k::delay_hist(dx, q->hist[h3].p, q->hist[(h3 + 1) % 3].p, n, (int)hl, e.stream);
+        q->front.mark(e.stream);
+        if (n > 0 && par) {
             if (!spec) q->ord.wait(e.stream);         // chunks near the start read the true state
             k::agc_spec_front(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
         }
-        if (n > 0) k::delay_hist(dx, q->hist[sl].p, q->hist[1 - sl].p, n, (int)hl, e.stream);
-        q->front.mark(e.stream);
         q->ord.wait(e.stream);
         if (n > 0) {
             if (par) {
