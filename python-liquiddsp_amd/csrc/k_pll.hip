@@ -707,6 +707,99 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
     prev.first = false;
 }
 
+// The F24 lane-block, hand-scheduled end to end.  x holds this lane-block's
+// offsets with every earlier repair applied; the next lane-block's (xn) are
+// formed from Kb, D before this block's repairs and carried through them in
+// the repair loop (two VALU ops per repair placed in the v_cmp -> s_and
+// shadow), so no lane-block starts with a multiply on its critical path.  The
+// interval test of the repaired lanes follows the loop in the same block.
+template <bool STATS>
+__device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int nv, WState& g, uint32_t S, PrevLB& prev,
+                                          const CandBuf& cb, const FullCtx& fc, const float* tab, float* y, int lane,
+                                          uint32_t& x, uint32_t e0nx, uint32_t sxn, float* yb)
+{
+    const uint32_t srel = E0.z;
+    const uint32_t W = (STATS && cb.dbg == 3) ? ~0u : E0.y;       // dbg 3: timing only, no repairs
+    uint32_t Kb = rfl(g.Kb), D = rfl(g.D);
+    const uint32_t Kb0 = Kb, D0 = D;
+    uint32_t xn, xp, t, off, j, dk1, dk2, nr;
+    unsigned long long mask, m0, PM, bad, bit, above;
+    // per repair: ff1, two readlanes, x += dk2' + srel dk1 (24-bit mad), the
+    // lane's post-repair x kept, the next events; Kb, D and the next
+    // lane-block's offsets follow in the shadow of the v_cmp.  Afterwards the
+    // interval test and the repaired outputs' store with exec = PM (empty when
+    // the test fails: walk_fallback then redoes the lane-block).
+    asm volatile(
+        "v_mul_lo_u32 %[t], %[d], %[sxn]\n\t"
+        "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
+        "v_add3_u32 %[xn], %[e0nx], %[kb], %[t]\n\t"
+        "v_mov_b32 %[xp], 0\n\t"
+        "v_lshlrev_b32 %[off], 2, %[sx]\n\t"
+        "s_mov_b64 %[pm], 0\n\t"
+        "s_mov_b64 %[m0], %[mask]\n\t"
+        "s_cmp_eq_u64 %[mask], 0\n\t"
+        "s_cbranch_scc1 2f\n"
+        "1:\n\t"
+        "s_ff1_i32_b64 %[j], %[mask]\n\t"
+        "v_readlane_b32 %[dk1], %[e1x], %[j]\n\t"
+        "v_readlane_b32 %[dk2], %[e1y], %[j]\n\t"
+        "s_lshl_b64 %[bit], 1, %[j]\n\t"
+        "s_lshl_b64 %[above], -2, %[j]\n\t"
+        "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
+        "v_add_u32 %[x], %[dk2], %[x]\n\t"
+        "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
+        "s_add_u32 %[d], %[d], %[dk1]\n\t"
+        "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
+        "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
+        "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
+        "s_and_b64 %[mask], %[mask], %[above]\n\t"
+        "s_cbranch_scc1 1b\n"
+        "2:\n\t"
+        "v_sub_u32 %[t], %[xp], %[lp]\n\t"
+        "v_cmp_gt_u32_e64 %[bad], %[t], %[span]\n\t"
+        "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"
+        "s_and_b64 %[bad], %[bad], %[pm]\n\t"
+        "s_cmp_eq_u64 %[bad], 0\n\t"
+        "s_cselect_b64 exec, %[pm], 0\n\t"
+        "global_store_dword %[off], %[out], %[yb]\n\t"
+        "s_mov_b64 exec, -1"
+        : [x] "+v"(x), [xn] "=&v"(xn), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [mask] "=&s"(mask),
+          [m0] "=&s"(m0), [pm] "=&s"(PM), [bad] "=&s"(bad), [kb] "+s"(Kb), [d] "+s"(D), [j] "=&s"(j),
+          [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [bit] "=&s"(bit), [above] "=&s"(above), [nr] "=&s"(nr)
+        : [e1x] "v"(E1.x), [e1y] "v"(E1.y), [sx] "v"(srel), [sxn] "v"(sxn), [e0nx] "v"(e0nx), [w] "v"(W),
+          [lp] "v"(E0.w), [span] "v"(E1.w), [out] "v"(E1.z), [yb] "s"(yb)
+        : "scc", "exec", "memory");
+    g.Kb = Kb;
+    g.D = D;
+    g.nrep += nr;                                // live counters (ldsp_ampmodem_walk_stats)
+    if (STATS && m0 != 0) {
+        g.nlb++;
+        g.nsame += PM == m0 ? 1u : 0u;
+    }
+    if (STATS && cb.dbg == 2 && nv > 0) bad = 1;
+    if (__builtin_expect(bad != 0, 0)) {         // (never in a padding lane-block: nv <= 0 there)
+        WState r = g;
+        r.Kb = Kb0;
+        r.D = D0;
+        r.nrep -= nr;
+        r.nfb++;
+        const long s_first = prev.first ? 0l : (long)prev.S + rl(prev.srel, prev.nv - 1) + 1;
+        r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, tab, y, lane);
+        g.Kb = rfl(r.Kb);
+        g.D = rfl(r.D);
+        g.nrep = rfl(r.nrep);
+        g.nfb = rfl(r.nfb);
+        xn = e0nx + g.Kb + sxn * g.D;
+    }
+    x = xn;
+    prev.srel = srel;
+    prev.nv = nv;
+    prev.S = S;
+    prev.first = false;
+}
+
 // Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + 3
 // into the LDS ring meanwhile.
 template <bool F24, bool STATS>
@@ -775,14 +868,33 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             // software-pipelined LDS reads: the next lane-block's entries are always
             // fetched (clamped), so every wait is the same lgkmcnt
             uint4 A0 = b.e[0][lane], A1 = b.e[1][lane];
+            if constexpr (F24) {
+                // entries two lane-blocks ahead: lane-block q + 1's E0 feeds q's asm.
+                // Straight-line over all 8 lane-blocks: the last block's tail is
+                // padded with W = ~0 (k_pll_entries), where nothing is ever repaired.
+                uint4 N0 = b.e[0][64 + lane], N1 = b.e[1][64 + lane];
+                uint32_t x = A0.x + g.Kb + A0.z * g.D;
+                float* yb = y + S;
 #pragma unroll
-            for (int q = 0; q < kBlkE / 64; q++) {
-                const int qn = min(q + 1, kBlkE / 64 - 1) * 64 + lane;
-                const uint4 N0 = b.e[0][qn], N1 = b.e[1][qn];
-                if (q * 64 >= cnt) break;
-                walk_lb<F24, STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane);
-                A0 = N0;
-                A1 = N1;
+                for (int q = 0; q < kBlkE / 64; q++) {
+                    const int qn = min(q + 2, kBlkE / 64 - 1) * 64 + lane;
+                    const uint4 M0 = b.e[0][qn], M1 = b.e[1][qn];
+                    walk_lb24<STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane, x, N0.x, N0.z, yb);
+                    A0 = N0;
+                    A1 = N1;
+                    N0 = M0;
+                    N1 = M1;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < kBlkE / 64; q++) {
+                    const int qn = min(q + 1, kBlkE / 64 - 1) * 64 + lane;
+                    const uint4 N0 = b.e[0][qn], N1 = b.e[1][qn];
+                    if (q * 64 >= cnt) break;
+                    walk_lb<F24, STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane);
+                    A0 = N0;
+                    A1 = N1;
+                }
             }
         }
         // LDS-only barrier: __syncthreads() would also drain the loaders' global fetch of

@@ -1,4 +1,9 @@
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "agc or amradio or smoke" > gpurun_out/pt.log 2>&1 || { tail -20 gpurun_out/pt.log; exit 1; }
-tail -1 gpurun_out/pt.log
-timeout -k 10 400 python scripts/block_sweep.py > gpurun_out/block_sweep.log 2>&1; rc=$?; grep streams gpurun_out/block_sweep.log | head -10; exit $rc
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+for m in 1 3; do
+  LDSP_DEBUG_PLL=$m timeout -k 10 300 python bench.py --steps 3 --warmup 1 --streams 1 --no-cpu-baseline --no-components > gpurun_out/pll_dbg$m.log 2>&1
+  rc=$?; echo "dbg$m rc=$rc"; grep "ldsp pll" gpurun_out/pll_dbg$m.log | tail -2
+  grep -o '"k_pll_walk": {[^}]*}' gpurun_out/pll_dbg$m.log
+  [ $rc -eq 0 ] || exit $rc
+done
