@@ -755,6 +755,54 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
         "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
         "s_and_b64 %[mask], %[mask], %[above]\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "s_ff1_i32_b64 %[j], %[mask]\n\t"
+        "v_readlane_b32 %[dk1], %[e1x], %[j]\n\t"
+        "v_readlane_b32 %[dk2], %[e1y], %[j]\n\t"
+        "s_lshl_b64 %[bit], 1, %[j]\n\t"
+        "s_lshl_b64 %[above], -2, %[j]\n\t"
+        "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
+        "v_add_u32 %[x], %[dk2], %[x]\n\t"
+        "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
+        "s_add_u32 %[d], %[d], %[dk1]\n\t"
+        "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
+        "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
+        "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
+        "s_and_b64 %[mask], %[mask], %[above]\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "s_ff1_i32_b64 %[j], %[mask]\n\t"
+        "v_readlane_b32 %[dk1], %[e1x], %[j]\n\t"
+        "v_readlane_b32 %[dk2], %[e1y], %[j]\n\t"
+        "s_lshl_b64 %[bit], 1, %[j]\n\t"
+        "s_lshl_b64 %[above], -2, %[j]\n\t"
+        "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
+        "v_add_u32 %[x], %[dk2], %[x]\n\t"
+        "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
+        "s_add_u32 %[d], %[d], %[dk1]\n\t"
+        "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
+        "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
+        "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
+        "s_and_b64 %[mask], %[mask], %[above]\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "s_ff1_i32_b64 %[j], %[mask]\n\t"
+        "v_readlane_b32 %[dk1], %[e1x], %[j]\n\t"
+        "v_readlane_b32 %[dk2], %[e1y], %[j]\n\t"
+        "s_lshl_b64 %[bit], 1, %[j]\n\t"
+        "s_lshl_b64 %[above], -2, %[j]\n\t"
+        "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
+        "v_add_u32 %[x], %[dk2], %[x]\n\t"
+        "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
+        "s_add_u32 %[d], %[d], %[dk1]\n\t"
+        "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
+        "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
+        "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
+        "s_and_b64 %[mask], %[mask], %[above]\n\t"
         "s_cbranch_scc1 1b\n"
         "2:\n\t"
         "v_sub_u32 %[t], %[xp], %[lp]\n\t"
