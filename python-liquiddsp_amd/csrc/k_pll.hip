@@ -716,22 +716,25 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
 template <bool STATS>
 __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int nv, WState& g, uint32_t S, PrevLB& prev,
                                           const CandBuf& cb, const FullCtx& fc, const float* tab, float* y, int lane,
-                                          uint32_t& x, uint32_t e0nx, uint32_t sxn, float* yb)
+                                          uint32_t& x, unsigned long long& mask, uint32_t e0nx, uint32_t sxn, uint32_t wn,
+                                          float* yb)
 {
     const uint32_t srel = E0.z;
     const uint32_t W = (STATS && cb.dbg == 3) ? ~0u : E0.y;       // dbg 3: timing only, no repairs
+    if (STATS && cb.dbg == 3) wn = ~0u;
     uint32_t Kb = rfl(g.Kb), D = rfl(g.D);
     const uint32_t Kb0 = Kb, D0 = D;
     uint32_t xn, xp, t, off, j, dk1, dk2, nr;
-    unsigned long long mask, m0, PM, bad, bit, above;
+    unsigned long long m0, PM, bad, bit, above;
     // per repair: ff1, two readlanes, x += dk2' + srel dk1 (24-bit mad), the
     // lane's post-repair x kept, the next events; Kb, D and the next
     // lane-block's offsets follow in the shadow of the v_cmp.  Afterwards the
     // interval test and the repaired outputs' store with exec = PM (empty when
-    // the test fails: walk_fallback then redoes the lane-block).
+    // the test fails: walk_fallback then redoes the lane-block).  mask: this
+    // lane-block's events on entry, the next lane-block's on exit (formed
+    // beside the interval test, so the two VALU -> SALU hand-offs overlap).
     asm volatile(
         "v_mul_lo_u32 %[t], %[d], %[sxn]\n\t"
-        "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
         "v_add3_u32 %[xn], %[e0nx], %[kb], %[t]\n\t"
         "v_mov_b32 %[xp], 0\n\t"
         "v_lshlrev_b32 %[off], 2, %[sx]\n\t"
@@ -805,6 +808,7 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "s_and_b64 %[mask], %[mask], %[above]\n\t"
         "s_cbranch_scc1 1b\n"
         "2:\n\t"
+        "v_cmp_gt_u32_e64 %[mask], %[xn], %[wn]\n\t"
         "v_sub_u32 %[t], %[xp], %[lp]\n\t"
         "v_cmp_gt_u32_e64 %[bad], %[t], %[span]\n\t"
         "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"
@@ -813,10 +817,10 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "s_cselect_b64 exec, %[pm], 0\n\t"
         "global_store_dword %[off], %[out], %[yb]\n\t"
         "s_mov_b64 exec, -1"
-        : [x] "+v"(x), [xn] "=&v"(xn), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [mask] "=&s"(mask),
+        : [x] "+v"(x), [xn] "=&v"(xn), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [mask] "+s"(mask),
           [m0] "=&s"(m0), [pm] "=&s"(PM), [bad] "=&s"(bad), [kb] "+s"(Kb), [d] "+s"(D), [j] "=&s"(j),
           [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [bit] "=&s"(bit), [above] "=&s"(above), [nr] "=&s"(nr)
-        : [e1x] "v"(E1.x), [e1y] "v"(E1.y), [sx] "v"(srel), [sxn] "v"(sxn), [e0nx] "v"(e0nx), [w] "v"(W),
+        : [e1x] "v"(E1.x), [e1y] "v"(E1.y), [sx] "v"(srel), [sxn] "v"(sxn), [e0nx] "v"(e0nx), [w] "v"(W), [wn] "v"(wn),
           [lp] "v"(E0.w), [span] "v"(E1.w), [out] "v"(E1.z), [yb] "s"(yb)
         : "scc", "exec", "memory");
     g.Kb = Kb;
@@ -840,6 +844,7 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         g.nrep = rfl(r.nrep);
         g.nfb = rfl(r.nfb);
         xn = e0nx + g.Kb + sxn * g.D;
+        mask = __builtin_amdgcn_ballot_w64(xn > wn);
     }
     x = xn;
     prev.srel = srel;
@@ -922,12 +927,14 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 // padded with W = ~0 (k_pll_entries), where nothing is ever repaired.
                 uint4 N0 = b.e[0][64 + lane], N1 = b.e[1][64 + lane];
                 uint32_t x = A0.x + g.Kb + A0.z * g.D;
+                unsigned long long mk = __builtin_amdgcn_ballot_w64(x > ((STATS && cb.dbg == 3) ? ~0u : A0.y));
                 float* yb = y + S;
 #pragma unroll
                 for (int q = 0; q < kBlkE / 64; q++) {
                     const int qn = min(q + 2, kBlkE / 64 - 1) * 64 + lane;
                     const uint4 M0 = b.e[0][qn], M1 = b.e[1][qn];
-                    walk_lb24<STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane, x, N0.x, N0.z, yb);
+                    walk_lb24<STATS>(A0, A1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane, x, mk, N0.x, N0.z,
+                                     N0.y, yb);
                     A0 = N0;
                     A1 = N1;
                     N0 = M0;

@@ -83,6 +83,35 @@ __global__ void __launch_bounds__(64) k_loop(const uint4* E, uint32_t* out, int 
                 x = x + sx * b1 + b2;
                 mask = __builtin_amdgcn_ballot_w64(x > W) & ((~0ull << j) << 1);
             } while (mask != 0);
+        } else if (V == 7 || V == 8) {   // the production asm loop (k_pll.hip walk_lb24), rolled / unrolled x4
+            uint32_t xn = x ^ 5u, j, dk1, dk2;
+            unsigned long long bit, above;
+#define WL_BODY \
+    "s_ff1_i32_b64 %[j], %[mask]\n\t" \
+    "v_readlane_b32 %[dk1], %[e1x], %[j]\n\t" \
+    "v_readlane_b32 %[dk2], %[e1y], %[j]\n\t" \
+    "s_lshl_b64 %[bit], 1, %[j]\n\t" \
+    "s_lshl_b64 %[above], -2, %[j]\n\t" \
+    "s_or_b64 %[pm], %[pm], %[bit]\n\t" \
+    "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t" \
+    "v_add_u32 %[x], %[dk2], %[x]\n\t" \
+    "s_add_u32 %[kb], %[kb], %[dk2]\n\t" \
+    "s_add_u32 %[d], %[d], %[dk1]\n\t" \
+    "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t" \
+    "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t" \
+    "v_mad_i32_i24 %[xn], %[sx], %[dk1], %[xn]\n\t" \
+    "v_add_u32 %[xn], %[dk2], %[xn]\n\t" \
+    "s_and_b64 %[mask], %[mask], %[above]\n\t"
+#define WL_OPS \
+    : [x] "+v"(x), [xn] "+v"(xn), [xp] "+v"(xpost), [mask] "+s"(mask), [pm] "+s"(PM), [kb] "+s"(Kb), [d] "+s"(D), \
+      [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [bit] "=&s"(bit), [above] "=&s"(above) \
+    : [e1x] "v"(d1), [e1y] "v"(d2), [sx] "v"(sx), [w] "v"(W) : "scc"
+            if (V == 7)
+                asm volatile("1:\n\t" WL_BODY "s_cbranch_scc1 1b" WL_OPS);
+            else
+                asm volatile("1:\n\t" WL_BODY "s_cbranch_scc0 2f\n\t" WL_BODY "s_cbranch_scc0 2f\n\t" WL_BODY
+                             "s_cbranch_scc0 2f\n\t" WL_BODY "s_cbranch_scc1 1b\n2:" WL_OPS);
+            acc += xn;
         } else if (V == 3) {     // pure SALU loop over the mask (no ballot per step)
             do {
                 const int j = __builtin_ctzll(mask);
@@ -124,19 +153,21 @@ int main()
     run(k_loop<4>, "V4 readlane + s_mov");
     run(k_loop<5>, "V5 LDS broadcast");
     run(k_loop<6>, "V6 ds_bpermute broadcast");
+    run(k_loop<7>, "V7 production asm, rolled");
+    run(k_loop<8>, "V8 production asm, unrolled x4");
     // s_memtime frequency: compare against wall clock
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
     hipEventRecord(a);
-    hipLaunchKernelGGL(k_loop<0>, dim3(1), dim3(64), 0, 0, dE, dout, nlb * 10, dclk);
+    hipLaunchKernelGGL(k_loop<8>, dim3(1), dim3(64), 0, 0, dE, dout, nlb * 10, dclk);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
     hipEventElapsedTime(&ms, a, b);
     unsigned long long c = 0;
     hipMemcpy(&c, dclk, 8, hipMemcpyDeviceToHost);
-    printf("V0 x10: %.3f ms wall, %llu ticks -> %.1f MHz memtime; %.2f ns per repair\n", ms, c, c / (ms * 1e3),
+    printf("V8 x10: %.3f ms wall, %llu ticks -> %.1f MHz memtime; %.2f ns per repair\n", ms, c, c / (ms * 1e3),
            ms * 1e6 / (64.0 * nlb * 10));
     return 0;
 }
