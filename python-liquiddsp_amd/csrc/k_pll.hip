@@ -725,7 +725,8 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     uint32_t Kb = rfl(g.Kb), D = rfl(g.D);
     const uint32_t Kb0 = Kb, D0 = D;
     uint32_t xn, xp, t, off, j, dk1, dk2, nr;
-    unsigned long long m0, PM, bad, bit, above;
+    unsigned long long PM, bad, bit, above;
+    const unsigned long long m0 = mask;          // (STATS only)
     // per repair: ff1, two readlanes, x += dk2' + srel dk1 (24-bit mad), the
     // lane's post-repair x kept, the next events; Kb, D and the next
     // lane-block's offsets follow in the shadow of the v_cmp.  Afterwards the
@@ -736,10 +737,8 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     asm volatile(
         "v_mul_lo_u32 %[t], %[d], %[sxn]\n\t"
         "v_add3_u32 %[xn], %[e0nx], %[kb], %[t]\n\t"
-        "v_mov_b32 %[xp], 0\n\t"
         "v_lshlrev_b32 %[off], 2, %[sx]\n\t"
         "s_mov_b64 %[pm], 0\n\t"
-        "s_mov_b64 %[m0], %[mask]\n\t"
         "s_cmp_eq_u64 %[mask], 0\n\t"
         "s_cbranch_scc1 2f\n"
         "1:\n\t"
@@ -818,7 +817,7 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "global_store_dword %[off], %[out], %[yb]\n\t"
         "s_mov_b64 exec, -1"
         : [x] "+v"(x), [xn] "=&v"(xn), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [mask] "+s"(mask),
-          [m0] "=&s"(m0), [pm] "=&s"(PM), [bad] "=&s"(bad), [kb] "+s"(Kb), [d] "+s"(D), [j] "=&s"(j),
+          [pm] "=&s"(PM), [bad] "=&s"(bad), [kb] "+s"(Kb), [d] "+s"(D), [j] "=&s"(j),
           [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [bit] "=&s"(bit), [above] "=&s"(above), [nr] "=&s"(nr)
         : [e1x] "v"(E1.x), [e1y] "v"(E1.y), [sx] "v"(srel), [sxn] "v"(sxn), [e0nx] "v"(e0nx), [w] "v"(W), [wn] "v"(wn),
           [lp] "v"(E0.w), [span] "v"(E1.w), [out] "v"(E1.z), [yb] "s"(yb)

@@ -1,9 +1,8 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
-for m in 1 3; do
-  LDSP_DEBUG_PLL=$m timeout -k 10 300 python bench.py --steps 3 --warmup 1 --streams 1 --no-cpu-baseline --no-components > gpurun_out/pll_dbg$m.log 2>&1
-  rc=$?; echo "dbg$m rc=$rc"; grep "ldsp pll" gpurun_out/pll_dbg$m.log | tail -2
-  grep -o '"k_pll_walk": {[^}]*}' gpurun_out/pll_dbg$m.log
-  [ $rc -eq 0 ] || exit $rc
-done
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "ampmodem or amradio or broadcast or smoke" > gpurun_out/pytest_pll.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -1 gpurun_out/pytest_pll.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 50 --no-cpu-baseline --no-components > gpurun_out/pll_bb.log 2>&1
+rc=$?; grep -o '"ms_per_step": [0-9.]*\|"ms_per_launch": [0-9.]*' gpurun_out/pll_bb.log | tr '\n' ' '; echo
+exit $rc
