@@ -222,6 +222,12 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void *x, size_t n, void *y
  * sample by sample.  All zero after a sequential (short) call.  Synchronises. */
 int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t *entries, uint64_t *repairs,
                              uint64_t *fallbacks);
+/* Diagnostics, no reference counterpart: the walker's entry margin B = 2^log2_b
+ * for the calls that follow (8..21; 0 restores the default).  A narrower
+ * margin leaves fewer entries and fails more gap proofs, so more lane-blocks
+ * are redone sample by sample -- the tests use it to exercise that path.
+ * Returns the previous setting. */
+int ldsp_debug_pll_margin(int log2_b);
 
 /* ------------------------------------------------------------------------
  * Broadcast AM demodulator.  Replaces BroadcastAM (src/demod.hpp:93-153,

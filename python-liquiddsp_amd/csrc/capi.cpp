@@ -1668,6 +1668,11 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
     });
 }
 
+int ldsp_debug_pll_margin(int log2_b)
+{
+    return k::pll_margin_override(log2_b);
+}
+
 int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t* entries, uint64_t* repairs, uint64_t* fallbacks)
 {
     return guard([&] {

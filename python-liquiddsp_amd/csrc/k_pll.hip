@@ -26,6 +26,7 @@
 //                block's records into an LDS double buffer meanwhile.
 // The result is bit-identical to the sequential loop (k_pll_seq, also used for
 // short calls); ~2 % of samples need a repair on locked AM signals.
+#include <atomic>
 #include <cstdlib>
 
 #include "kernels.hpp"
@@ -119,7 +120,7 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
 // ------------------------------------------------------------------ candidates
 // Candidate chunks of kCand samples.  Per sample the candidate kernel writes
 // its output to y and a record (AoS, 2 x uint4 = 32 B):
-//   R0 = (w = theta + 2^21, dk1(i-1), dk2(i-1), dk1(i+1)),  R1 = (dk2(i+1), out(i-1), out(i+1), 0)
+//   R0 = (w = theta + 2^21, dk1(i-1), dk2(i-1), dk1(i+1)),  R1 = (dk2(i+1), out(i-1), out(i+1), out(i))
 // (dk = kick at table index i -+ 1 minus kick at the candidate's index i),
 // and per chunk its start / end state and its entry count (see the walker).
 constexpr int kBlkE = 512;        // walker block: entries
@@ -193,7 +194,8 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
                     const Kick km = pll_eval(tab, (ic - 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
                     const Kick kp = pll_eval(tab, (ic + 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
                     cb.rec[2 * s] = make_uint4(w, km.k1 - kc.k1, km.k2 - kc.k2, kp.k1 - kc.k1);
-                    cb.rec[2 * s + 1] = make_uint4(kp.k2 - kc.k2, __float_as_uint(km.out), __float_as_uint(kp.out), 0u);
+                    cb.rec[2 * s + 1] = make_uint4(kp.k2 - kc.k2, __float_as_uint(km.out), __float_as_uint(kp.out),
+                                                 __float_as_uint(kc.out));
                     y[s] = kc.out;
                     nent += (risky(w, cb.B) || s == a || s == b - 1) ? 1u : 0u;
                 }
@@ -852,6 +854,113 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     prev.first = false;
 }
 
+// ---- The whole walker block (8 lane-blocks of 64 entries) as one asm statement.
+// Entries go straight from the LDS ring into v100-v163 (lane-block q: E0 in
+// v[100+8q : 103+8q], E1 in v[104+8q : 107+8q]); each lane-block is the
+// repair loop of walk_lb24 (the next lane-block's offsets carried through it)
+// followed by the store of its repaired outputs with exec = PM -- before the
+// interval test is known.  The test itself is folded lane-wise into acc
+// (saturating x_post - L' - span over the repaired lanes), so no scalar
+// instruction waits on it; one ballot at the end says whether any repaired
+// lane of the block failed.  Then the caller restores the candidates' outputs
+// (record R1.w) at every entry of the block and redoes it lane-block by
+// lane-block from its entry state (walk_lb24, with walk_fallback where needed).
+#define WB_REP(E1X, E1Y, SX, W, SXN, X, XN)                                                                  \
+    "s_ff1_i32_b64 %[j], %[mask]\n\t"                                                                      \
+    "v_readlane_b32 %[dk1], " E1X ", %[j]\n\t"                                                             \
+    "v_readlane_b32 %[dk2], " E1Y ", %[j]\n\t"                                                             \
+    "s_lshl_b64 %[bit], 1, %[j]\n\t"                                                                       \
+    "s_lshl_b64 %[above], -2, %[j]\n\t"                                                                    \
+    "s_or_b64 %[pm], %[pm], %[bit]\n\t"                                                                    \
+    "v_mad_i32_i24 " X ", " SX ", %[dk1], " X "\n\t"                                                       \
+    "v_add_u32 " X ", %[dk2], " X "\n\t"                                                                   \
+    "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
+    "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
+    "v_cmp_gt_u32_e64 %[mask], " X ", " W "\n\t"                                                           \
+    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
+    "v_mad_i32_i24 " XN ", " SXN ", %[dk1], " XN "\n\t"                                                    \
+    "v_add_u32 " XN ", %[dk2], " XN "\n\t"                                                                 \
+    "s_and_b64 %[mask], %[mask], %[above]\n\t"
+// lane-block Q: KC = lgkmcnt that has its own entries and the next one's E0 landed
+#define WB_LB(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN)                           \
+    "s_waitcnt lgkmcnt(" KC ")\n\t"                                                                        \
+    "v_mul_lo_u32 %[t], %[d], " N0Z "\n\t"                                                                 \
+    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
+    "v_lshlrev_b32 %[off], 2, " E0Z "\n\t"                                                                 \
+    "s_mov_b64 %[pm], 0\n\t"                                                                               \
+    "s_cmp_eq_u64 %[mask], 0\n\t"                                                                          \
+    "s_cbranch_scc1 2f\n"                                                                                  \
+    "1:\n\t"                                                                                               \
+    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
+    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
+    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
+    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc1 1b\n"                                           \
+    "2:\n\t"                                                                                               \
+    "v_cmp_gt_u32_e64 %[mask], " XN ", " N0Y "\n\t"                                                        \
+    "v_sub_u32 %[t], %[xp], " E0W "\n\t"                                                                   \
+    "s_mov_b64 exec, %[pm]\n\t"                                                                            \
+    "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
+    "s_mov_b64 exec, -1\n\t"                                                                               \
+    "v_cndmask_b32_e64 %[t], 0, %[t], %[pm]\n\t"                                                           \
+    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
+    "v_or_b32 %[acc], %[acc], %[t]\n\t"                                                                    \
+    "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
+    "s_add_u32 %[nrep], %[nrep], %[nr]\n\t"
+#define WB_LBQ(Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN)                                            \
+    WB_LB(Q, KC, "v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN)
+
+// Returns nonzero when a repaired lane of the block failed its interval test.
+__device__ __forceinline__ bool walk_blk8(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep,
+                                          uint32_t& srel7)
+{
+    uint32_t xa, xb, xp, t, off, acc, j, dk1, dk2, nr;
+    unsigned long long mask, pm, bad, bit, above;
+    asm volatile(
+        "ds_read_b128 v[100:103], %[la]\n\t"
+        "ds_read_b128 v[104:107], %[la] offset:8192\n\t"
+        "ds_read_b128 v[108:111], %[la] offset:1024\n\t"
+        "ds_read_b128 v[112:115], %[la] offset:9216\n\t"
+        "ds_read_b128 v[116:119], %[la] offset:2048\n\t"
+        "ds_read_b128 v[120:123], %[la] offset:10240\n\t"
+        "ds_read_b128 v[124:127], %[la] offset:3072\n\t"
+        "ds_read_b128 v[128:131], %[la] offset:11264\n\t"
+        "ds_read_b128 v[132:135], %[la] offset:4096\n\t"
+        "ds_read_b128 v[136:139], %[la] offset:12288\n\t"
+        "ds_read_b128 v[140:143], %[la] offset:5120\n\t"
+        "ds_read_b128 v[144:147], %[la] offset:13312\n\t"
+        "ds_read_b128 v[148:151], %[la] offset:6144\n\t"
+        "ds_read_b128 v[152:155], %[la] offset:14336\n\t"
+        "ds_read_b128 v[156:159], %[la] offset:7168\n\t"
+        "ds_read_b128 v[160:163], %[la] offset:15360\n\t"
+        "v_mov_b32 %[acc], 0\n\t"
+        "s_waitcnt lgkmcnt(15)\n\t"
+        "v_mul_lo_u32 %[t], %[d], v102\n\t"
+        "v_add3_u32 %[xa], v100, %[kb], %[t]\n\t"
+        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n\t"
+        WB_LBQ("0", "13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]")
+        WB_LBQ("1", "11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]")
+        WB_LBQ("2", "9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]")
+        WB_LBQ("3", "7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]")
+        WB_LBQ("4", "5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]")
+        WB_LBQ("5", "3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]")
+        WB_LBQ("6", "1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]")
+        WB_LBQ("7", "0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]")
+        "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"
+        "v_mov_b32 %[s7], v158"
+        : [xa] "=&v"(xa), [xb] "=&v"(xb), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [s7] "=&v"(srel7),
+          [mask] "=&s"(mask), [pm] "=&s"(pm), [bad] "=&s"(bad), [bit] "=&s"(bit), [above] "=&s"(above),
+          [kb] "+s"(Kb), [d] "+s"(D), [nrep] "+s"(nrep), [acc] "=&v"(acc),
+          [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr)
+        : [la] "v"(lds), [yb] "s"(yb)
+        : "scc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
+          "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
+          "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135",
+          "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148",
+          "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161",
+          "v162", "v163");
+    return bad != 0;
+}
+
 // Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + 3
 // into the LDS ring meanwhile.
 template <bool F24, bool STATS>
@@ -920,7 +1029,39 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             // software-pipelined LDS reads: the next lane-block's entries are always
             // fetched (clamped), so every wait is the same lgkmcnt
             uint4 A0 = b.e[0][lane], A1 = b.e[1][lane];
-            if constexpr (F24) {
+            if constexpr (F24 && !STATS) {
+                float* yb = y + S;
+                const uint32_t Kb0 = rfl(g.Kb), D0 = rfl(g.D), nrep0 = rfl(g.nrep);
+                uint32_t Kb = Kb0, D = D0, nrep = nrep0, s7;
+                const bool bad = walk_blk8((uint32_t)(uintptr_t)&b.e[0][lane], yb, Kb, D, nrep, s7);
+                g.Kb = Kb;
+                g.D = D;
+                g.nrep = nrep;
+                if (__builtin_expect(bad, 0)) {
+                    // undo the block's speculative stores (candidate outputs at every
+                    // entry), then redo it lane-block by lane-block from its entry state
+                    // (each rewrite of a sample lands after the previous one: vmcnt(0))
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    for (int q = 0; q < kBlkE / 64; q++) {
+                        const uint32_t sr = b.e[0][q * 64 + lane].z;
+                        if (q * 64 + lane < cnt) y[S + sr] = __uint_as_float(cb.rec[2 * ((long)S + sr) + 1].w);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    g.Kb = Kb0;
+                    g.D = D0;
+                    g.nrep = nrep0;
+                    for (int q = 0; q < kBlkE / 64; q++) {
+                        const uint4 C0 = b.e[0][q * 64 + lane], C1 = b.e[1][q * 64 + lane];
+                        const uint4 N0 = b.e[0][min(q + 1, kBlkE / 64 - 1) * 64 + lane];
+                        uint32_t x = C0.x + g.Kb + C0.z * g.D;
+                        unsigned long long mk = __builtin_amdgcn_ballot_w64(x > C0.y);
+                        walk_lb24<false>(C0, C1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane, x, mk, N0.x,
+                                         N0.z, N0.y, yb);
+                    }
+                } else {
+                    prev = PrevLB{s7, min(64, cnt - (kBlkE - 64)), S, false};
+                }
+            } else if constexpr (F24) {
                 // entries two lane-blocks ahead: lane-block q + 1's E0 feeds q's asm.
                 // Straight-line over all 8 lane-blocks: the last block's tail is
                 // padded with W = ~0 (k_pll_entries), where nothing is ever repaired.
@@ -1056,6 +1197,8 @@ static PllIn pll_in(const PllCall& c)
     return in;
 }
 
+static std::atomic<int> g_margin_override{0};    // ldsp_debug_pll_margin
+
 static CandBuf cand_buf(const PllCall& c)
 {
     const PllLayout L = pll_layout(c.n);
@@ -1081,11 +1224,17 @@ static CandBuf cand_buf(const PllCall& c)
     // crossings, |f| often exceeds 2^20 there, and gap proofs would fail: B = 2^21
     // makes every sample an entry (no gaps; 11 ms instead of 190 ms per 1.6 M
     // samples of locked DSB-SC, scripts/pll_stress.py).
-    static const int lb = std::getenv("LDSP_PLL_LOGB") ? std::atoi(std::getenv("LDSP_PLL_LOGB")) : 0;
+    static const int lb_env = std::getenv("LDSP_PLL_LOGB") ? std::atoi(std::getenv("LDSP_PLL_LOGB")) : 0;
+    const int lb = g_margin_override.load() ? g_margin_override.load() : lb_env;
     cb.B = 1u << std::max(8, std::min(21, lb ? lb : (c.costas ? 21 : 19)));
     static const int dbg = std::getenv("LDSP_DEBUG_PLL") ? std::atoi(std::getenv("LDSP_DEBUG_PLL")) : 0;
     cb.dbg = dbg;
     return cb;
+}
+
+int pll_margin_override(int log2_b)
+{
+    return g_margin_override.exchange(log2_b);
 }
 
 void pll_front(const PllCall& c, hipStream_t s)

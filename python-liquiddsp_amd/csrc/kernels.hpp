@@ -176,6 +176,7 @@ bool pll_parallel(size_t n);
 // the candidate chunks.  Reads only the guess state, never the true state, so
 // it may run while the previous call's pll_back is still walking.
 void pll_front(const PllCall& c, hipStream_t s);
+int pll_margin_override(int log2_b);       // diagnostics: 0 = default; returns the previous value
 // Back half: the exact walk over the candidates (or the sequential loop);
 // reads and advances the true state, so it must follow the previous call's back half.
 void pll_back(const PllCall& c, hipStream_t s);

@@ -907,6 +907,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         check(ldsp_debug_math_eval(fn, (const float*)a, (const float*)b, (float*)y, n, (void*)stream));
     });
     // per-kernel device timing (ldsp_profile_*): {kernel: (calls, total_ms)}
+    m.def("_debug_pll_margin", [](int lb) { return ldsp_debug_pll_margin(lb); });
     m.def("_profile_enable", [](bool on) { check(ldsp_profile_enable(on ? 1 : 0)); });
     m.def("_profile_reset", [] { check(ldsp_profile_reset()); });
     m.def("_profile_report", [] {

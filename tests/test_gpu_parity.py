@@ -450,6 +450,27 @@ def test_ampmodem_walk_stats(ld, ora, rng):
     assert g._walk_stats()[0] >= 0
 
 
+@pytest.mark.parametrize("log2_b", [18, 17])
+def test_ampmodem_walk_fallbacks(ld, ora, rng, log2_b):
+    # A narrower walker margin (2^19 by default) leaves gaps whose proofs fail:
+    # those lane-blocks are redone sample by sample (walk_fallback) and the rest
+    # of their walker block continues one lane-block at a time.  Output and final
+    # state must stay bit-identical.
+    x = _am(rng, 400_000, 48000.0, 300.0, amp=1.0)
+    o = ora.AmpModem(0.5, "dsb", carrier=True)
+    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
+    prev = ld._debug_pll_margin(log2_b)
+    try:
+        y = g(x)
+        stats = g._walk_stats()
+    finally:
+        ld._debug_pll_margin(prev)
+    assert_bitwise(y, o(x))
+    assert g.pll_state() == o.pll_state
+    entries, repairs, fallbacks = stats
+    assert fallbacks > 0 and repairs > 0
+
+
 @pytest.mark.parametrize("carrier", [True, False])
 def test_ampmodem_parallel_calls_on_two_streams(ld, ora, rng, carrier):
     # Long calls run as candidates + walker; consecutive calls alternate torch
