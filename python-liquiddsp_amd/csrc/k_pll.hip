@@ -451,6 +451,22 @@ constexpr int kLoadWaves = kWalkThreads / 64 - 1;             // 7
 constexpr int kPieces = 2 * kBlkE * 16 / 1024;                // 16 x 1 KiB per block
 constexpr int kDmaPer = (kPieces + kLoadWaves - 1) / kLoadWaves + 1;   // 3 pieces + the block header
 static_assert(kDmaPer == 4, "walker DMA wait counts below assume 4 DMAs per loader wave per block");
+constexpr int kRing = 8;             // LDS ring of walker blocks (8 x 16 KiB), DMA'd kRing - 1 ahead
+
+// Loader wave: wait until at most k blocks' DMAs (kDmaPer each) are still in flight.
+__device__ __forceinline__ void vm_wait_blocks(long k)
+{
+    switch (k <= 0 ? 0 : (k >= kRing - 2 ? kRing - 2 : (int)k)) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    }
+}
+static_assert(kRing == 8, "vm_wait_blocks covers up to 6 blocks in flight");
 
 // M0 is compiler-reserved: save / set / restore it inside one statement
 // (cdna_hip_programming.md LDS-DMA recipe); asm loads are invisible to hipcc's
@@ -961,13 +977,13 @@ __device__ __forceinline__ bool walk_blk8(uint32_t lds, float* yb, uint32_t& Kb,
     return bad != 0;
 }
 
-// Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + 3
+// Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + kRing - 1
 // into the LDS ring meanwhile.
 template <bool F24, bool STATS>
 __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, CandBuf cb,
                                                            float* __restrict__ y)
 {
-    __shared__ WalkBufE buf[4];          // ring: block c in buf[c & 3], DMA'd three blocks ahead
+    __shared__ WalkBufE buf[kRing];      // ring: block c in buf[c % kRing], DMA'd kRing - 1 blocks ahead
     __shared__ float wtab[1024];         // NCO table for the fallback's full loop steps
     // Own the CU: 8 waves x 256 VGPRs fill every SIMD's register file, so no wave of
     // the kernels running beside the walk (the next call's AGC, candidates, ...)
@@ -980,11 +996,9 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     const uint32_t NE = rfl(*(volatile uint32_t*)cb.ne);
     const long nblk = ((long)NE + kBlkE - 1) / kBlkE;
     if (wave != 0) {
-        for (long b0 = 0; b0 < 3 && b0 < nblk; b0++) walk_dma(buf[b0], cb, b0, lw, lane);
-        // block 0 landed: at most the DMAs of blocks 1 and 2 still in flight
-        if (nblk > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (nblk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (long b0 = 0; b0 < kRing - 1 && b0 < nblk; b0++) walk_dma(buf[b0], cb, b0, lw, lane);
+        // block 0 landed: at most the DMAs of blocks 1 .. kRing - 2 still in flight
+        vm_wait_blocks(nblk - 1);
     }
     for (int i = tid; i < 1024; i += kWalkThreads) wtab[i] = in.table[i];
     __syncthreads();
@@ -1014,14 +1028,12 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     for (long c = 0; c < nblk; c++) {
         const unsigned long long t0 = STATS ? wall_clock64() : 0;
         if (wave != 0) {
-            // slot (c + 3) & 3 held block c - 1, released by the previous barrier
-            if (c + 3 < nblk) walk_dma(buf[(c + 3) & 3], cb, c + 3, lw, lane);
+            // slot (c + kRing - 1) % kRing held block c - 1, released by the previous barrier
+            if (c + kRing - 1 < nblk) walk_dma(buf[(c + kRing - 1) % kRing], cb, c + kRing - 1, lw, lane);
             // block c + 1 must have landed before the barrier below publishes it
-            if (c + 3 < nblk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if (c + 2 < nblk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            vm_wait_blocks(nblk - c - 2);
         } else {
-            const WalkBufE& b = buf[c & 3];
+            const WalkBufE& b = buf[c % kRing];
             const uint32_t Sn = rfl(b.hdr[0]);
             g.Kb += (Sn - S) * g.D;
             S = Sn;
