@@ -30,10 +30,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# One dependent repair of the PLL walk (ballot -> s_ff1 -> 2 readlanes -> 24-bit
-# multiply-add -> compare), measured alone on MI355X by scripts/ubench/walk_loop.hip
-# (125 shader cycles at 2.4 GHz): the serial floor of the walker per repair.
-REPAIR_FLOOR_NS = 52.2
+# One dependent repair of the PLL walk (s_ff1 -> 2 readlanes -> 24-bit multiply-add
+# -> compare -> s_and), the walker's own loop (unrolled x4) measured alone on MI355X by
+# scripts/ubench/walk_loop.hip (V8: 108.6 shader cycles at 2.39 GHz): the serial
+# floor of the walker per repair.
+REPAIR_FLOOR_NS = 45.4
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector spec
 
 
