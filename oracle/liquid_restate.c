@@ -31,8 +31,10 @@
  *    (liquid >= 1.5 "Variant F");
  *  - NCO: 1024-entry sine table, index ((theta + 2^21) >> 22) & 1023;
  *  - dot products: the portable C dotprod (sequential accumulation from the
- *    oldest sample, no FMA); SIMD builds of liquid sum in another order;
+ *    oldest sample, no FMA); SIMD builds of liquid sum in another order,
+ *    modelled by -DORA_DOTPROD_LANES=8 (a bounding variant, oracle/variants.py);
  *  - transcendentals inside feedback loops: ora_math.h (fdlibm algorithms);
+ *    -DORA_USE_LIBM=1 calls the system libm (glibc) instead (variant);
  *  - complex division in the filter designs: C's `/` on _Complex operands,
  *    i.e. libgcc __divsc3 / __divdc3.  This library is linked by gcc 11, whose
  *    static libgcc implements Smith's method; newer libgcc_s (also present in
@@ -220,6 +222,10 @@ static inline const float *win_read(const ora_window *w)
     return w->buf + (size_t)w->pos * w->ncomp;
 }
 
+#ifndef ORA_DOTPROD_LANES
+#define ORA_DOTPROD_LANES 0
+#endif
+#if ORA_DOTPROD_LANES == 0
 /* liquid dotprod (portable C, dotprod_*.proto.c run/run4): sequential sum
  * r = 0; r += h[i]*x[i], i = 0..n-1 (x oldest first), real taps. */
 static inline float dot_rr(const float *h, const float *x, unsigned int n)
@@ -253,6 +259,78 @@ static inline void dot_cc(const float *h, const float *x, unsigned int n, float 
     y[0] = rr;
     y[1] = ri;
 }
+#else
+/* SIMD-order model of liquid's x86 dotprod (dotprod_*.sse.c / .avx.c): the
+ * float stream is multiplied and accumulated ORA_DOTPROD_LANES floats at a time
+ * into one vector register of partial sums (lane j holds the terms j, j + W,
+ * j + 2W, ...), the register is reduced pairwise ((s0 + s1) + (s2 + s3)) ...
+ * as hadd does, and the tail of n mod W floats is added sequentially.  For
+ * complex data the stream is the interleaved (re, im) floats, so the even
+ * lanes carry the real part and the odd lanes the imaginary part.  A bounding
+ * variant (oracle/variants.py): which SIMD kernel a given liquid build uses
+ * is a configure-time choice. */
+#define ORA_W ORA_DOTPROD_LANES
+static inline float ora_hsum(const float *a, unsigned int w, unsigned int stride)
+{
+    /* pairwise tree over lanes 0, stride, 2 stride, ... (w / stride of them) */
+    float t[16];
+    unsigned int m = w / stride, i;
+    for (i = 0; i < m; i++) t[i] = a[i * stride];
+    while (m > 1) {
+        for (i = 0; i < m / 2; i++) t[i] = t[2 * i] + t[2 * i + 1];
+        m /= 2;
+    }
+    return t[0];
+}
+static inline float dot_rr(const float *h, const float *x, unsigned int n)
+{
+    float acc[ORA_W];
+    unsigned int i, j, t = n - n % ORA_W;
+    for (j = 0; j < ORA_W; j++) acc[j] = 0.0f;
+    for (i = 0; i < t; i += ORA_W)
+        for (j = 0; j < ORA_W; j++) acc[j] += h[i + j] * x[i + j];
+    float r = ora_hsum(acc, ORA_W, 1);
+    for (; i < n; i++) r += h[i] * x[i];
+    return r;
+}
+static inline void dot_cr(const float *h, const float *x, unsigned int n, float *y)
+{
+    /* taps duplicated [h0 h0 h1 h1 ...] against [x0r x0i x1r x1i ...] */
+    float acc[ORA_W];
+    unsigned int nf = 2 * n, i, j, t = nf - nf % ORA_W;
+    for (j = 0; j < ORA_W; j++) acc[j] = 0.0f;
+    for (i = 0; i < t; i += ORA_W)
+        for (j = 0; j < ORA_W; j++) acc[j] += h[(i + j) / 2] * x[i + j];
+    float rr = ora_hsum(acc, ORA_W, 2), ri = ora_hsum(acc + 1, ORA_W, 2);
+    for (; i < nf; i += 2) {
+        rr += h[i / 2] * x[i];
+        ri += h[i / 2] * x[i + 1];
+    }
+    y[0] = rr;
+    y[1] = ri;
+}
+static inline void dot_cc(const float *h, const float *x, unsigned int n, float *y)
+{
+    /* (re, im) pairs: real lanes accumulate ac - bd, imaginary lanes ad + bc */
+    float acc[ORA_W];
+    unsigned int nf = 2 * n, i, j, t = nf - nf % ORA_W;
+    for (j = 0; j < ORA_W; j++) acc[j] = 0.0f;
+    for (i = 0; i < t; i += ORA_W)
+        for (j = 0; j < ORA_W; j += 2) {
+            float a = h[i + j], b = h[i + j + 1], c = x[i + j], d = x[i + j + 1];
+            acc[j] += a * c - b * d;
+            acc[j + 1] += a * d + b * c;
+        }
+    float rr = ora_hsum(acc, ORA_W, 2), ri = ora_hsum(acc + 1, ORA_W, 2);
+    for (; i < nf; i += 2) {
+        float a = h[i], b = h[i + 1], c = x[i], d = x[i + 1];
+        rr += a * c - b * d;
+        ri += a * d + b * c;
+    }
+    y[0] = rr;
+    y[1] = ri;
+}
+#endif
 
 /* ===================================================================== */
 /* firfilt: liquid src/filter/src/firfilt.proto.c                         */

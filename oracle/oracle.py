@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import subprocess
+import sys
 
 import numpy as np
 
@@ -152,6 +153,35 @@ def _load():
 
 
 _lib = None
+
+# Build variants of the restatement (oracle/Makefile): which libm the feedback
+# loops call and which order liquid's dotprod sums in are platform choices of a
+# liquid-dsp build, so "liquid's output" is a family; variants.py records how
+# far apart its members are.  "default" is the variant the GPU exact mode
+# reproduces bit for bit.
+VARIANTS = {
+    "default": "libliquid_restate.so",
+    "libm": "libliquid_restate_libm.so",
+    "simd": "libliquid_restate_simd.so",
+    "libm_simd": "libliquid_restate_libm_simd.so",
+}
+_variant_mods = {}
+
+
+def variant(name: str):
+    """This module bound to another build variant of the restatement (a separate
+    module instance with its own library; same classes and functions)."""
+    if name == "default" and not globals().get("_VARIANT"):
+        return sys.modules[__name__]
+    if name not in _variant_mods:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location(f"oracle_variant_{name}", os.path.abspath(__file__))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        mod._LIB_PATH = os.path.join(_HERE, "_build", VARIANTS[name])
+        mod._VARIANT = name
+        _variant_mods[name] = mod
+    return _variant_mods[name]
 
 
 def lib():

@@ -22,6 +22,20 @@
 namespace ldsp {
 
 static thread_local std::string g_last_error;
+
+#ifdef LDSP_TUNING
+long knob_env(const char* name, long dflt)
+{
+    const char* v = std::getenv(name);
+    return v ? std::atol(v) : dflt;
+}
+double knob_env_f(const char* name, double dflt)
+{
+    const char* v = std::getenv(name);
+    return v ? std::atof(v) : dflt;
+}
+const char* knob_env_s(const char* name) { return std::getenv(name); }
+#endif
 void set_last_error(const std::string& m) { g_last_error = m; }
 
 int current_device()
@@ -55,9 +69,30 @@ struct Exec {
     bool host;
 };
 
-static Exec make_exec(int device, int mem, void* stream)
+// The device a call's buffers live on.  A device-memory call runs on the
+// device that holds its input (made current for the call, so an object's first
+// call binds it there); a host-memory call on the current device.
+struct BufDevice {
+    int dev;
+    DeviceGuard g;
+    static int of(int mem, const void* x)
+    {
+        if (mem == LDSP_MEM_DEVICE && x) {
+            hipPointerAttribute_t a;
+            if (hipPointerGetAttributes(&a, x) == hipSuccess && a.type == hipMemoryTypeDevice) return a.device;
+            (void)hipGetLastError();
+        }
+        return current_device();
+    }
+    BufDevice(int mem, const void* x) : dev(of(mem, x)), g(dev) {}
+};
+
+static Exec make_exec(int device, int mem, void* stream, const BufDevice& bd)
 {
     LDSP_REQUIRE(mem == LDSP_MEM_HOST || mem == LDSP_MEM_DEVICE, "mem must be LDSP_MEM_HOST or LDSP_MEM_DEVICE");
+    if (mem == LDSP_MEM_DEVICE && bd.dev != device)
+        throw Error(LDSP_EINVAL, "buffer on device " + std::to_string(bd.dev) + " but the object lives on device " +
+                                     std::to_string(device) + " (objects are bound to the device of their first call)");
     Exec e;
     e.device = device;
     e.host = (mem == LDSP_MEM_HOST);
@@ -724,7 +759,7 @@ std::vector<std::pair<std::string, std::pair<long, double>>> g_done;   // name -
 hipEvent_t g_t0 = nullptr;
 void drain_locked()
 {
-    static const char* tl_path = std::getenv("LDSP_PROF_TIMELINE");
+    static const char* tl_path = LDSP_KNOB_S("LDSP_PROF_TIMELINE");
     FILE* tl = tl_path ? std::fopen(tl_path, "a") : nullptr;
     for (auto& r : g_pending) {
         float ms = 0.0f;
@@ -894,6 +929,7 @@ int ldsp_firfilt_reset(ldsp_firfilt_t q)
         DeviceGuard g(q->device);
         const size_t bytes = std::max<size_t>(q->h.size() - 1, 1) * q->esz();
         for (auto& b : q->hist) LDSP_HIP(hipMemsetAsync(b.p, 0, bytes, q->last));
+        q->ord.mark(q->last);              // a call on another stream waits for the zeroing
     });
 }
 
@@ -946,9 +982,10 @@ int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "firfilt_execute: NULL buffer");
+        const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         q->ord.wait(e.stream);
         const size_t bytes = n * q->esz();
         const void* dx = q->stg.dev_in(e, x, bytes);
@@ -1037,6 +1074,7 @@ int ldsp_resamp_reset(ldsp_resamp_t q)
         DeviceGuard g(q->device);
         const size_t bytes = std::max<size_t>(q->sub_len - 1, 1) * q->esz();
         for (auto& b : q->hist) LDSP_HIP(hipMemsetAsync(b.p, 0, bytes, q->last));
+        q->ord.mark(q->last);              // a call on another stream waits for the zeroing
     });
 }
 
@@ -1078,9 +1116,10 @@ int ldsp_resamp_execute(ldsp_resamp_t q, const void* x, size_t n, void* y, size_
         if (K > cap) throw Error(LDSP_ERANGE, "resamp_execute: output capacity too small");
         LDSP_REQUIRE(n == 0 || x, "resamp_execute: NULL input");
         LDSP_REQUIRE(K == 0 || y, "resamp_execute: NULL output");
+        const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         q->ord.wait(e.stream);
         const void* dx = q->stg.dev_in(e, x, n * q->esz());
         void* dy = q->stg.dev_out(e, y, K * q->esz());
@@ -1184,9 +1223,10 @@ int ldsp_nco_mix(ldsp_nco_t q, const void* x, size_t n, void* y, int down, int m
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "nco_mix: NULL buffer");
+        const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         void* dy = q->stg.dev_out(e, y, n * 8);
         k::nco_mix(dx, dy, n, q->theta, q->dtheta, q->dtab.as<float>(), down != 0, q->type, e.stream);
@@ -1282,6 +1322,7 @@ int ldsp_iirfilt_reset(ldsp_iirfilt_t q)
         DeviceGuard g(q->device);
         LDSP_HIP(hipMemsetAsync(q->st32.p, 0, q->st32.cap, q->last));
         LDSP_HIP(hipMemsetAsync(q->st64.p, 0, q->st64.cap, q->last));
+        q->ord.mark(q->last);              // a call on another stream waits for the zeroing
     });
 }
 
@@ -1341,9 +1382,10 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "iirfilt_execute: NULL buffer");
+        const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         q->ord.wait(e.stream);
         const size_t bytes = n * (q->cplx ? 8 : 4);
         const void* dx = q->stg.dev_in(e, x, bytes);
@@ -1363,7 +1405,7 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
             } else if (q->mode == LDSP_MODE_EXACT) {
                 q->state_to(false, e.stream);
                 k::iir_seq(q->cplx, d, dx, n, q->st32.as<float>(), dy, e.stream);
-            } else if (q->D <= k::kIirBlkMaxD && !std::getenv("LDSP_IIR_OLDSCAN")) {
+            } else if (q->D <= k::kIirBlkMaxD && !LDSP_KNOB("LDSP_IIR_OLDSCAN", 0)) {
                 q->state_to(true, e.stream);
                 const k::IirBlkPlan p = q->blk_plan(n);
                 k::iir_blk(q->cplx, d, q->b.data(), q->a.data(), dx, n, q->st64.as<double>(), p, dy, e.stream);
@@ -1515,9 +1557,10 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "agc_execute: NULL buffer");
+        const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         const int sl = (int)(q->ncall & 1), h3 = (int)(q->ncall % 3);
         q->slot[sl].wait(e.stream);
         q->front.wait(e.stream);
@@ -1534,10 +1577,10 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         // (k_agc.hip); measured on the AM chain at bandwidth 0.01 the exact loop then
         // coalesces within ~110 samples on average, 2834 at worst.
         const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
-        static const float wmul = std::getenv("LDSP_AGC_WMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WMUL")) : 20.0f;
-        static const float wamul = std::getenv("LDSP_AGC_WAMUL") ? (float)std::atof(std::getenv("LDSP_AGC_WAMUL")) : 40.0f;
-        static const int rounds = std::getenv("LDSP_AGC_ROUNDS") ? std::atoi(std::getenv("LDSP_AGC_ROUNDS")) : 3;
-        static const bool nospec = std::getenv("LDSP_AGC_NOSPEC") != nullptr;   // A/B: every call from the true state
+        static const float wmul = LDSP_KNOB_F("LDSP_AGC_WMUL", 20.0f);
+        static const float wamul = LDSP_KNOB_F("LDSP_AGC_WAMUL", 40.0f);
+        static const int rounds = LDSP_KNOB("LDSP_AGC_ROUNDS", 3);
+        static const bool nospec = LDSP_KNOB("LDSP_AGC_NOSPEC", 0) != 0;   // A/B: every call from the true state
         const int W = (int)std::min(1 << 18, std::max(256, (int)(wmul / a)));
         const int Wa = (int)std::min(1 << 20, std::max(1024, (int)(wamul / a)));
         const long hl = (long)W + Wa + k::kAgcPow;
@@ -1549,7 +1592,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         const bool spec = !nospec && q->hist_valid >= hl;
         // chunk-parallel once it beats the one-lane loop: its latency is Wa approximate + W + 256
         // exact steps (~1.6 ms at bandwidth 0.01) against ~0.57 us per sample sequentially
-        static const size_t parmin = std::getenv("LDSP_AGC_PARMIN") ? (size_t)std::atol(std::getenv("LDSP_AGC_PARMIN")) : 0;
+        static const size_t parmin = (size_t)LDSP_KNOB("LDSP_AGC_PARMIN", 0L);
         const bool par = n >= (parmin ? parmin : (size_t)(0.7 * (0.16 * Wa + 0.43 * (W + 256)) / 0.57) + 256);
         k::SpecPlan p;
         if (n > 0 && par) {
@@ -1572,7 +1615,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         q->ord.wait(e.stream);
         if (n > 0) {
             if (par) {
-                static const bool dbg = std::getenv("LDSP_DEBUG_AGC") != nullptr;
+                static const bool dbg = LDSP_KNOB("LDSP_DEBUG_AGC", 0) != 0;
                 if (dbg) {
                     p.dbg = (unsigned*)p.scratch + (size_t)p.nchunks * 8;
                     LDSP_HIP(hipMemsetAsync(p.dbg, 0, 8 * sizeof(unsigned), e.stream));
@@ -1732,7 +1775,8 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     q->ord.wait(e.stream);
     k::pll_back(c, e.stream);
     if (!par) q->front.mark(e.stream);
-    if (par && std::getenv("LDSP_DEBUG_PLL")) {
+    static const bool dbg_pll = LDSP_KNOB("LDSP_DEBUG_PLL", 0) != 0;
+    if (par && dbg_pll) {
         unsigned long long stt[7];
         LDSP_HIP(hipMemcpyAsync(stt, (char*)c.scratch + k::pll_stats_offset(n), sizeof(stt), hipMemcpyDeviceToHost,
                                 e.stream));
@@ -1758,9 +1802,10 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "ampmodem_demodulate: NULL buffer");
+        const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
         if (n > 0) {
@@ -1835,9 +1880,10 @@ int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void* x, size_t n, void* y, 
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "bcastam_demodulate: NULL buffer");
+        const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
         if (n > 0) {
@@ -1897,13 +1943,14 @@ int ldsp_freqdem_demodulate(ldsp_freqdem_t q, const void* x, size_t n, void* y, 
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "freqdem_demodulate: NULL buffer");
+        const BufDevice bd(mem, x);
         if (q->device < 0) {
             const int dev = current_device();
             for (int i = 0; i < 2; i++) zero_now(q->prev[i].ensure(8, dev), 0, 8);
             q->device = dev;
         }
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         q->ord.wait(e.stream);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
@@ -1960,13 +2007,14 @@ int ldsp_delay_execute(ldsp_delay_t q, const void* x, size_t n, int cplx, void* 
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "delay_execute: NULL buffer");
+        const BufDevice bd(mem, x);
         if (q->device < 0) {
             q->device = current_device();
             DeviceGuard g(q->device);
             q->zero();
         }
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         q->ord.wait(e.stream);
         const size_t es = cplx ? 8 : 4;
         const void* dx = q->stg.dev_in(e, x, n * es);
@@ -2080,6 +2128,7 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
         if (2 * k > cap) throw Error(LDSP_ERANGE, "fmstereo_execute: output capacity too small");
         LDSP_REQUIRE(n == 0 || x, "fmstereo_execute: NULL input");
         LDSP_REQUIRE(k == 0 || y, "fmstereo_execute: NULL output");
+        const BufDevice bd(mem, x);
         if (q->device < 0) {
             const int dev = current_device();
             q->dst.ensure(sizeof(k::FmState), dev);
@@ -2088,7 +2137,7 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
             q->device = dev;
         }
         DeviceGuard g(q->device);
-        const Exec e = make_exec(q->device, mem, stream);
+        const Exec e = make_exec(q->device, mem, stream, bd);
         q->ord.wait(e.stream);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, 2 * k * 4);
@@ -2126,8 +2175,9 @@ int ldsp_bytes_to_iq(const void* in, size_t nbytes, void* y, int mem, void* stre
     return guard([&] {
         const size_t n = nbytes / 4;
         LDSP_REQUIRE(n == 0 || (in && y), "bytes_to_iq: NULL buffer");
-        const int dev = current_device();
-        const Exec e = make_exec(dev, mem, stream);
+        const BufDevice bd(mem, in);
+        const int dev = bd.dev;
+        const Exec e = make_exec(dev, mem, stream, bd);
         std::unique_lock<std::mutex> lk(mu, std::defer_lock);
         if (e.host) lk.lock();   // the staging buffers are shared by host-memory calls
         if ((int)stgs.size() <= dev) stgs.resize(dev + 1);

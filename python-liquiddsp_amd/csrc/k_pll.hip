@@ -1193,7 +1193,7 @@ void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m
 // Candidates + walk beat the one-lane loop (~0.57 us per sample) from about two
 // thousand samples: their latency is the warm-up plus one recorded chunk
 // (~0.94 ms), then the walk.
-static const size_t kParMin = std::getenv("LDSP_PLL_PARMIN") ? (size_t)std::atol(std::getenv("LDSP_PLL_PARMIN")) : 2048;
+static const size_t kParMin = (size_t)LDSP_KNOB("LDSP_PLL_PARMIN", 2048L);
 bool pll_parallel(size_t n) { return n >= kParMin; }
 
 static PllIn pll_in(const PllCall& c)
@@ -1236,10 +1236,10 @@ static CandBuf cand_buf(const PllCall& c)
     // crossings, |f| often exceeds 2^20 there, and gap proofs would fail: B = 2^21
     // makes every sample an entry (no gaps; 11 ms instead of 190 ms per 1.6 M
     // samples of locked DSB-SC, scripts/pll_stress.py).
-    static const int lb_env = std::getenv("LDSP_PLL_LOGB") ? std::atoi(std::getenv("LDSP_PLL_LOGB")) : 0;
+    static const int lb_env = LDSP_KNOB("LDSP_PLL_LOGB", 0);
     const int lb = g_margin_override.load() ? g_margin_override.load() : lb_env;
     cb.B = 1u << std::max(8, std::min(21, lb ? lb : (c.costas ? 21 : 19)));
-    static const int dbg = std::getenv("LDSP_DEBUG_PLL") ? std::atoi(std::getenv("LDSP_DEBUG_PLL")) : 0;
+    static const int dbg = LDSP_KNOB("LDSP_DEBUG_PLL", 0);
     cb.dbg = dbg;
     return cb;
 }
@@ -1263,7 +1263,7 @@ void pll_front(const PllCall& c, hipStream_t s)
     const CandBuf cb = cand_buf(c);
     {
         LDSP_PROF(s, "k_pll_cand");
-        static const int warm = std::getenv("LDSP_PLL_WARM") ? std::atoi(std::getenv("LDSP_PLL_WARM")) : kWarm;
+        static const int warm = LDSP_KNOB("LDSP_PLL_WARM", kWarm);
         hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s, pll_in(c), (long)c.n,
                            c.st, c.gcur, cb, c.y, warm, c.costas);
     }
@@ -1307,7 +1307,7 @@ void pll_back(const PllCall& c, hipStream_t s)
     }
     {
         LDSP_PROF(s, "k_pll_walk");
-        static const bool stats = std::getenv("LDSP_DEBUG_PLL") != nullptr;
+        static const bool stats = LDSP_KNOB("LDSP_DEBUG_PLL", 0) != 0;
         const dim3 g(1), blk(kWalkThreads);
         const PllIn in = pll_in(c);
         const CandBuf cb = cand_buf(c);

@@ -131,6 +131,23 @@ struct StreamMark {
     }
 };
 
+// Tuning and diagnostic environment knobs (warm-up lengths, walker margin,
+// debug counters, timeline dumps) are read only by a tuning build
+// (`make TUNING=1`, -DLDSP_TUNING); the product library reads no environment
+// and always uses the default.
+#ifdef LDSP_TUNING
+long knob_env(const char* name, long dflt);
+double knob_env_f(const char* name, double dflt);
+const char* knob_env_s(const char* name);
+#define LDSP_KNOB(name, dflt) ((decltype(dflt))::ldsp::knob_env(name, (long)(dflt)))
+#define LDSP_KNOB_F(name, dflt) ((decltype(dflt))::ldsp::knob_env_f(name, (double)(dflt)))
+#define LDSP_KNOB_S(name) (::ldsp::knob_env_s(name))
+#else
+#define LDSP_KNOB(name, dflt) (dflt)
+#define LDSP_KNOB_F(name, dflt) (dflt)
+#define LDSP_KNOB_S(name) ((const char*)nullptr)
+#endif
+
 int current_device();                       // throws LDSP_EHIP when no GPU is present
 hipStream_t library_stream(int device);     // per-device non-blocking stream for host-memory calls
 

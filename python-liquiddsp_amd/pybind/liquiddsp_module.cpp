@@ -568,37 +568,38 @@ struct AmpModem {
         if (q) ldsp_ampmodem_destroy(q);
         q = nullptr;
     }
+    // makeFromArgs (demod.hpp:298-306): a known type string is recorded, an
+    // unknown one leaves mType unchanged and demodulates DSB.
     void make(float mod, const std::string& type, bool car)
     {
+        ldsp_ampmodem_t nq = nullptr;
         int mt = 0;
         auto it = kAmpTypes.find(type);
-        if (it != kAmpTypes.end()) {
-            mType = type;
-            mt = it->second;
-        }
-        check(ldsp_ampmodem_create(mod, mt, car ? 0 : 1, &q));
+        if (it != kAmpTypes.end()) mt = it->second;
+        check(ldsp_ampmodem_create(mod, mt, car ? 0 : 1, &nq));
+        if (it != kAmpTypes.end()) mType = type;
+        destroy();
+        q = nq;
     }
+    // The setters rebuild the modem (state reset, demod.hpp:250-276).  The new
+    // handle is created first and swapped in only on success, so a setter that
+    // fails (e.g. 'usb', not implemented) leaves the object and its settings
+    // unchanged instead of without a modem.
     void set_type(const std::string& type)
     {
-        if (type == "dsb" || type == "usb" || type == "lsb") {
-            mType = type;
-            destroy();
-            make(mModulation, mType, mCarrier);
-        }
+        if (type == "dsb" || type == "usb" || type == "lsb") make(mModulation, type, mCarrier);
     }
     std::string get_type() { return mType; }
     void set_modulation(float m)
     {
+        make(m, mType, mCarrier);
         mModulation = m;
-        destroy();
-        make(mModulation, mType, mCarrier);
     }
     float get_modulation() { return mModulation; }
     void set_carrier(bool c)
     {
+        make(mModulation, mType, c);
         mCarrier = c;
-        destroy();
-        make(mModulation, mType, mCarrier);
     }
     bool get_carrier() { return mCarrier; }
     void reset() { check(ldsp_ampmodem_reset(q)); }

@@ -94,6 +94,8 @@ def main():
     x = am_signal(8192)
     fi = O.IIRFilter(prototype=("cheby2", "lowpass", O.FMT_SOS, 8, 15000 / 2e6, 0.0, 0.1, 60.0), cplx=True)
     g["iir_B"], g["iir_A"], g["iir_x"], g["iir_y"] = Bs, As_, x, fi(x)
+    fi.reset()
+    g["iir_y64"] = fi.execute_f64(x)          # the same recursion in float64 (SURVEY 8(d) truth), rounded once
     meta["cases"]["iir"] = "iirfilt_crcf cheby2 lowpass order 8 fc 0.0075 Ap 0.1 As 60 (SOS)"
 
     # De-emphasis (DeemphasisFilter(48000)), real

@@ -7,8 +7,8 @@ the fixture's golden.json).
   * GPU: the MI355X kernels reproduce the stored outputs -- bit for bit in the
     exact modes and for every kernel whose fast mode is exact (resampler, NCO,
     AGC, AmpModem, de-emphasis); the fast FIR within 1e-6 relative; the fast
-    IIR (float64 scan) within 1e-3 relative of the float32 recursion (the
-    recursion's own rounding error for this narrow cheby2).
+    IIR (float64 scan) within 1e-6 of the float64 recursion and no further from
+    it than the float32 recursion is.
 """
 import json
 import os
@@ -70,6 +70,8 @@ def test_oracle_reproduces_iir_agc_ampmodem_chain(ora):
     same(A, G["iir_A"])
     f = ora.IIRFilter(sos=(G["iir_B"], G["iir_A"]), cplx=True)
     same(f(G["iir_x"]), G["iir_y"])
+    f.reset()
+    same(f.execute_f64(G["iir_x"]), G["iir_y64"])
     d = ora.IIRFilter(tf=(G["deemph_b"], G["deemph_a"]), cplx=False)
     same(d(G["deemph_x"]), G["deemph_y"])
     agc = ora.AGC()
@@ -121,8 +123,11 @@ def test_gpu_golden_iir(ld):
     same(np.float32(A), G["iir_A"])
     g.exact = True
     same(g(G["iir_x"]), G["iir_y"])
+    # fast mode (float64 scan): SURVEY 8(d) -- within 1e-6 of the float64 truth,
+    # and no further from it than the float32 recursion
     fast = ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2e6, Ap=0.1, As=60.0)
-    assert maxrel(fast(G["iir_x"]), G["iir_y"]) < 1e-3
+    err_gpu, err_f32 = maxrel(fast(G["iir_x"]), G["iir_y64"]), maxrel(G["iir_y"], G["iir_y64"])
+    assert err_gpu <= 1e-6 and err_gpu <= err_f32, (err_gpu, err_f32)
     d = ld.DeemphasisFilter(48000)
     same(d(G["deemph_x"]), G["deemph_y"])
 

@@ -651,17 +651,8 @@ def test_amradio_two_streams_bitwise(ld, ora, rng):
     assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), ora.AMRadio()(x))
 
 
-def test_amradio_fast_close(ld, ora, rng):
-    # Fast mode: the IIR stage is the float64 scan (more accurate than liquid's
-    # float32 recursion); the reference here evaluates that stage in float64 too.
-    # Rare 1-ulp differences of the IIR output perturb the PLL's 10-bit phase
-    # table index downstream, so the chain agrees to ~1e-5, not bit for bit.
-    x = _am(rng, 1 << 20, 2e6, 1200.0, amp=0.1)
-    run = _chain(ld, exact=False)
-    y = run(x)
-    ref = ora.AMRadio(iir_f64=True)(x)
-    assert len(y) == len(ref)
-    assert maxrel(y, ref) < 1e-3
+# (the fast-mode chain gate lives in tests/test_gpu_chain.py, beside the
+# benchmarked-configuration test)
 
 
 def test_device_tensor_path_matches_numpy(ld, ora, rng):
