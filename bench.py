@@ -22,7 +22,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # serialise.
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 32:
     os.environ["GPU_MAX_HW_QUEUES"] = "32"
-for p in (REPO, os.path.join(REPO, "python-liquiddsp_amd")):
+# LDSP_PKG_DIR: load the liquiddsp package from another build of it (e.g. the
+# tuning build of python-liquiddsp_amd/Makefile); default: the in-tree product.
+PKG_DIR = os.environ.get("LDSP_PKG_DIR") or os.path.join(REPO, "python-liquiddsp_amd")
+for p in (REPO, PKG_DIR):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -612,10 +612,10 @@ struct AmpObj {
     bool dev_newer = false;
     hipStream_t last = nullptr;
     // Cross-stream order (ldsp_common.hpp): `front` = end of a call's front half
-    // (lowpass + delay histories, candidate guess state), `ord` = end of a call
-    // (true PLL state, DC-blocker history), `slot[i]` = end of the last call that
-    // used scratch slot i.
-    StreamMark front, ord, slot[2];
+    // (lowpass + delay histories, candidate guess state), `ord` = end of a call's
+    // walk (true PLL state), `post` = end of its DC blocker (history),
+    // `slot[i]` = end of the last call that used scratch slot i.
+    StreamMark front, ord, post, slot[2];
     Staging stg;
     void reset_host()
     {
@@ -631,6 +631,7 @@ struct AmpObj {
     void sync_all()
     {
         ord.sync();
+        post.sync();
         front.sync();
         for (auto& sm : slot) sm.sync();
     }
@@ -1608,19 +1609,22 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         // the next call's history first: its front then waits for this copy only
         if (n > 0) k::delay_hist(dx, q->hist[h3].p, q->hist[(h3 + 1) % 3].p, n, (int)hl, e.stream);
         q->front.mark(e.stream);
+        static const bool dbg = LDSP_KNOB("LDSP_DEBUG_AGC", 0) != 0;    // per-round re-run counters
         if (n > 0 && par) {
+            if (dbg) {
+                p.dbg = (unsigned*)p.scratch + (size_t)p.nchunks * 8;
+                LDSP_HIP(hipMemsetAsync(p.dbg, 0, 8 * sizeof(unsigned), e.stream));
+            }
             if (!spec) q->ord.wait(e.stream);         // chunks near the start read the true state
             k::agc_spec_front(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
+            // speculative call: the repair rounds need no true state (off the chain between calls)
+            if (spec) k::agc_spec_repair(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
         }
         q->ord.wait(e.stream);
         if (n > 0) {
             if (par) {
-                static const bool dbg = LDSP_KNOB("LDSP_DEBUG_AGC", 0) != 0;
-                if (dbg) {
-                    p.dbg = (unsigned*)p.scratch + (size_t)p.nchunks * 8;
-                    LDSP_HIP(hipMemsetAsync(p.dbg, 0, 8 * sizeof(unsigned), e.stream));
-                }
-                k::agc_spec_back(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
+                if (spec) k::agc_spec_verify(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
+                else k::agc_spec_back(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
                 if (dbg) {
                     unsigned c[8];
                     LDSP_HIP(hipMemcpyAsync(c, p.dbg, sizeof(c), hipMemcpyDeviceToHost, e.stream));
@@ -1774,6 +1778,7 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     if (par) q->front.mark(e.stream);     // the sequential loop writes the guess itself: mark after it
     q->ord.wait(e.stream);
     k::pll_back(c, e.stream);
+    q->ord.mark(e.stream);                // the true PLL state: the next call's walk may start
     if (!par) q->front.mark(e.stream);
     static const bool dbg_pll = LDSP_KNOB("LDSP_DEBUG_PLL", 0) != 0;
     if (par && dbg_pll) {
@@ -1790,7 +1795,6 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
 
 static void amp_call_end(AmpObj* q, const Exec& e)
 {
-    q->ord.mark(e.stream);
     q->slot[q->ncall & 1].mark(e.stream);
     q->ncall++;
     q->cur = 1 - q->cur;
@@ -1811,9 +1815,14 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
         if (n > 0) {
             const int L = 2 * (int)q->m + 1;
             float* mbuf = amp_pll_stage(q, e, dx, n, q->mod_index, q->suppressed ? 1 : 0, q->suppressed ? dy : nullptr);
-            if (!q->suppressed)
+            if (!q->suppressed) {
+                // the DC blocker is off the walker's chain: the next call's walk
+                // waits for this walk only (ord), the next DC blocker for this one
+                q->post.wait(e.stream);
                 k::fir_exact(false, mbuf, q->dch[q->cur].p, q->dch[1 - q->cur].p, n, q->ddc.as<float>(), L, 1.0f,
                              dy, e.stream);
+                q->post.mark(e.stream);
+            }
             amp_call_end(q, e);
         }
         q->last = e.stream;

@@ -165,6 +165,7 @@ __device__ __forceinline__ void agc_run(AgcReg& r, const AgcState& p, const X& x
 __global__ void __launch_bounds__(64) k_agc_seq(const float2* __restrict__ x, long n, AgcState* st,
                                                 float2* __restrict__ y, uint8_t* __restrict__ status)
 {
+    LDSP_LATENCY_CRITICAL();
     constexpr int kS = 2048;
     __shared__ float2 xs[kS];
     const AgcState p = *st;
@@ -202,6 +203,7 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
                                                    unsigned* __restrict__ sc, float2* __restrict__ y,
                                                    uint8_t* __restrict__ status)
 {
+    LDSP_LATENCY_CRITICAL();
     const long chunk = (long)blockIdx.x * 64 + threadIdx.x;
     if (chunk >= nch) return;
     const AgcState p = *st;
@@ -288,6 +290,7 @@ __global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x,
                                                    const unsigned long long* __restrict__ flags,
                                                    float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg)
 {
+    LDSP_LATENCY_CRITICAL();
     const long k = (long)blockIdx.x * 64 + threadIdx.x;
     if (k >= nch || !agc_flag(flags, k) || (k > 0 && agc_flag(flags, k - 1))) return;
     const AgcState p = *st;
@@ -322,13 +325,17 @@ __global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x,
 
 // Parallel pre-check: bit c of flags[c / 64] = chunk c's start state differs
 // from chunk c-1's end state (after the repair rounds).
-// spec: every chunk started from a guess (chunk 0 is compared with the true state).
+// spec: 1 = every chunk started from a guess (chunk 0 is compared with the true
+// state); 2 = the same, but chunk 0 is presumed right (repair rounds that run
+// before the previous call has produced the true state; k_agc_verify then
+// checks chunk 0 directly).
 __global__ void __launch_bounds__(64) k_agc_flags(int C, int W, long nch, const unsigned* __restrict__ sc,
                                                   const AgcState* st, int spec, unsigned long long* __restrict__ flags)
 {
+    LDSP_LATENCY_CRITICAL();
     const long kk = (long)blockIdx.x * 64 + threadIdx.x;
     bool bad = false;
-    if (kk < nch && (spec ? true : (kk >= 1 && kk * C - W > 0))) {
+    if (kk < nch && (spec == 2 ? kk >= 1 : spec ? true : (kk >= 1 && kk * C - W > 0))) {
 #pragma unroll
         for (int i = 0; i < 4; i++) bad |= sc[kk * 8 + i] != pred_word(sc, st, kk, i);
     }
@@ -341,11 +348,14 @@ __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x,
                                                    const unsigned long long* __restrict__ flags, float2* __restrict__ y,
                                                    uint8_t* __restrict__ status, unsigned* dbg)
 {
+    LDSP_LATENCY_CRITICAL();
     const int lane = threadIdx.x;
     const AgcState p = *st;
     const long nw = (nch + 63) / 64;
     long k = spec ? 0 : 1;
-    bool direct = false;          // chunk k's predecessor was re-run: compare states, not its flag
+    // chunk k's predecessor was re-run, or (spec 2) chunk 0 was presumed right by
+    // the repair rounds: compare states, not the flag
+    bool direct = spec == 2;
     while (k < nch) {
         long kb;
         if (direct) {
@@ -443,10 +453,9 @@ void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, vo
     LDSP_HIP(hipGetLastError());
 }
 
-void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
+static void agc_rounds(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, int spec,
+                       hipStream_t s)
 {
-    if (n == 0) return;
-    const int spec = p.H > 0 ? 1 : 0;
     unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
     const unsigned nb = (unsigned)((p.nchunks + 63) / 64);
     for (int round = 0; round <= p.rounds; round++) {
@@ -465,6 +474,12 @@ void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, voi
         }
         LDSP_HIP(hipGetLastError());
     }
+}
+
+static void agc_verify(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, int spec,
+                       hipStream_t s)
+{
+    unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
     {
         LDSP_PROF(s, "k_agc_verify");
         hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, spec,
@@ -472,6 +487,28 @@ void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, voi
                            p.dbg ? p.dbg + p.rounds : nullptr);
     }
     LDSP_HIP(hipGetLastError());
+}
+
+void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
+{
+    if (n == 0) return;
+    const int spec = p.H > 0 ? 1 : 0;
+    agc_rounds(x, n, st, p, y, status, spec, s);
+    agc_verify(x, n, st, p, y, status, spec, s);
+}
+
+void agc_spec_repair(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
+                     hipStream_t s)
+{
+    if (n == 0) return;
+    agc_rounds(x, n, st, p, y, status, 2, s);
+}
+
+void agc_spec_verify(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
+                     hipStream_t s)
+{
+    if (n == 0) return;
+    agc_verify(x, n, st, p, y, status, 2, s);
 }
 
 void math_eval(int fn, const float* a, const float* b, float* y, size_t n, hipStream_t s)

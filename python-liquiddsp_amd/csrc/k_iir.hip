@@ -108,6 +108,7 @@ __device__ __forceinline__ int fstate_size(const IirDesc& d) { return d.sos ? 3 
 __global__ void k_iir_seq(IirDesc d, const float* __restrict__ x, long n, int ncomp, float* __restrict__ state,
                           float* __restrict__ y)
 {
+    LDSP_LATENCY_CRITICAL();
     const int c = threadIdx.x;
     if (c >= ncomp) return;
     float* st = state + c * fstate_size(d);
@@ -173,6 +174,7 @@ __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* 
                                                         const float* __restrict__ state0, int C, int W, long nch,
                                                         float* __restrict__ sc, float* __restrict__ y)
 {
+    LDSP_LATENCY_CRITICAL();
     const long ch = (long)blockIdx.x * 64 + threadIdx.x;
     if (ch >= nch * ncomp) return;
     const long chunk = ch / ncomp;
@@ -231,6 +233,7 @@ __global__ void __launch_bounds__(64) k_iir_spec_flags(IirDesc d, int ncomp, int
                                                        const float* __restrict__ sc,
                                                        unsigned long long* __restrict__ flags)
 {
+    LDSP_LATENCY_CRITICAL();
     const int fs = fstate_size(d);
     const int per = ncomp * fs;
     const long kk = (long)blockIdx.x * 64 + threadIdx.x;
@@ -251,6 +254,7 @@ __global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* 
                                                         const unsigned long long* __restrict__ flags,
                                                         float* __restrict__ state, float* __restrict__ y)
 {
+    LDSP_LATENCY_CRITICAL();
     const int lane = threadIdx.x;
     const int fs = fstate_size(d);
     const int per = ncomp * fs;   // floats per (chunk, kind)
@@ -463,6 +467,7 @@ __global__ void __launch_bounds__(1024) k_iir_scan_carry(int ncomp, long nch, in
                                                          const double* __restrict__ state0,
                                                          const double* __restrict__ Lc, double* __restrict__ carry)
 {
+    LDSP_LATENCY_CRITICAL();
     extern __shared__ __attribute__((aligned(16))) double sh[];   // [1024][D]
     const int t = threadIdx.x;
     const long c0 = (long)t * G;

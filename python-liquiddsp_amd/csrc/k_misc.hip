@@ -79,6 +79,7 @@ __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, lon
                                                 const float* __restrict__ table, float* __restrict__ lo,
                                                 float* __restrict__ ro)
 {
+    LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
     __shared__ float sb[2][kFmChunk];
     __shared__ float ub[2][kFmChunk];

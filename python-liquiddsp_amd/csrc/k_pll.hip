@@ -86,6 +86,7 @@ constexpr int kSeqChunk = 2048;
 template <bool COSTAS>
 __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st, int gcur, float* __restrict__ y)
 {
+    LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
     __shared__ float2 b0[kSeqChunk], b1[kSeqChunk];
     const int tid = threadIdx.x;
@@ -183,6 +184,13 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
                 n1[j] = *x1_ptr(in, ii);
             }
         }
+        // REC: the group's records and outputs are kept in registers and stored
+        // back to back after it, so each lane's 256 B of records and 32 B of
+        // outputs reach L2 as whole lines (stored one sample at a time, ~1 us
+        // apart, the partly written lines were evicted by the streaming kernels
+        // beside this one and reached HBM 3-4 times over).
+        uint4 r0[kB], r1[kB];
+        float yo[kB];
 #pragma unroll
         for (int j = 0; j < kB; j++) {
             if (i + j < b) {
@@ -193,14 +201,33 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
                     const uint32_t w = theta + (1u << 21);
                     const Kick km = pll_eval(tab, (ic - 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
                     const Kick kp = pll_eval(tab, (ic + 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
-                    cb.rec[2 * s] = make_uint4(w, km.k1 - kc.k1, km.k2 - kc.k2, kp.k1 - kc.k1);
-                    cb.rec[2 * s + 1] = make_uint4(kp.k2 - kc.k2, __float_as_uint(km.out), __float_as_uint(kp.out),
-                                                 __float_as_uint(kc.out));
-                    y[s] = kc.out;
+                    r0[j] = make_uint4(w, km.k1 - kc.k1, km.k2 - kc.k2, kp.k1 - kc.k1);
+                    r1[j] = make_uint4(kp.k2 - kc.k2, __float_as_uint(km.out), __float_as_uint(kp.out),
+                                       __float_as_uint(kc.out));
+                    yo[j] = kc.out;
                     nent += (risky(w, cb.B) || s == a || s == b - 1) ? 1u : 0u;
                 }
                 d += kc.k1;
                 theta += kc.k2 + d;
+            }
+        }
+        if (REC) {
+            if (i + kB <= b) {
+#pragma unroll
+                for (int j = 0; j < kB; j++) {
+                    cb.rec[2 * (i + j)] = r0[j];
+                    cb.rec[2 * (i + j) + 1] = r1[j];
+                }
+#pragma unroll
+                for (int j = 0; j < kB; j++) y[i + j] = yo[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < kB; j++)
+                    if (i + j < b) {
+                        cb.rec[2 * (i + j)] = r0[j];
+                        cb.rec[2 * (i + j) + 1] = r1[j];
+                        y[i + j] = yo[j];
+                    }
             }
         }
     }
@@ -216,6 +243,7 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
 __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st, int gcur, CandBuf cb,
                                                  float* __restrict__ y, int warm, int from_true)
 {
+    LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
     for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = in.table[i];
     __syncthreads();
@@ -250,6 +278,7 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st,
 // turned by half a turn, so every candidate sits in chunk 0's branch.
 __global__ void __launch_bounds__(64) k_pll_reflip(PllIn in, long n, AmpState* st, CandBuf cb, float* __restrict__ y)
 {
+    LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
     for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = in.table[i];
     __syncthreads();
@@ -305,6 +334,7 @@ __device__ __forceinline__ uint32_t half_flip(uint32_t dth, int flip)
 
 __global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
 {
+    LDSP_LATENCY_CRITICAL();
     __shared__ uint32_t sa[1024], sb[1024], sc[1024], sh[1024];
     const int t = threadIdx.x;
     const long per = (cb.nchc + 1023) / 1024;
@@ -370,6 +400,7 @@ __global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
 // The tail of the last walker block is padded with W = ~0 (never an event).
 __global__ void __launch_bounds__(256) k_pll_entries(CandBuf cb, long n)
 {
+    LDSP_LATENCY_CRITICAL();
     const int lane = threadIdx.x & 63;
     const long k = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= cb.nchc) return;
@@ -983,6 +1014,7 @@ template <bool F24, bool STATS>
 __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, CandBuf cb,
                                                            float* __restrict__ y)
 {
+    LDSP_LATENCY_CRITICAL();
     __shared__ WalkBufE buf[kRing];      // ring: block c in buf[c % kRing], DMA'd kRing - 1 blocks ahead
     __shared__ float wtab[1024];         // NCO table for the fallback's full loop steps
     // Own the CU: 8 waves x 256 VGPRs fill every SIMD's register file, so no wave of
@@ -1137,6 +1169,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
 __global__ void k_delay_hist(const float2* __restrict__ x, const float2* __restrict__ hist, float2* __restrict__ hist_out,
                              long n, int m)
 {
+    LDSP_LATENCY_CRITICAL();
     for (int j = threadIdx.x; j < m; j += blockDim.x) {
         const long g = n - m + j;
         hist_out[j] = g >= 0 ? x[g] : hist[g + m];

@@ -139,6 +139,16 @@ void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, vo
                     hipStream_t s);
 void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
                    hipStream_t s);
+// A speculative call's back half in two parts: the repair rounds over chunks
+// 1.. (chunk 0 presumed right: they read only the chunk records, so they may
+// run while the previous call is still producing the true state), then -- after
+// it -- the verifier, which checks chunk 0 against the true state, re-runs
+// whatever the rounds left and advances the state: the only AGC work on the
+// chain from one call to the next.
+void agc_spec_repair(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
+                     hipStream_t s);
+void agc_spec_verify(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status,
+                     hipStream_t s);
 // hist_out = the last m samples of (hist, x[0, n)) (complex), for the next call.
 void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m, hipStream_t s);
 

@@ -148,6 +148,12 @@ const char* knob_env_s(const char* name);
 #define LDSP_KNOB_S(name) ((const char*)nullptr)
 #endif
 
+// Serial-latency kernels (the one-lane loops, chunk warm-ups, the PLL walk,
+// single-workgroup scans) share SIMDs with the streaming kernels of other
+// calls in flight; the highest wave priority lets their dependent chains issue
+// first instead of by wave age (MI355X_MICROARCH.md, two waves per SIMD, item 2).
+#define LDSP_LATENCY_CRITICAL() __builtin_amdgcn_s_setprio(3)
+
 int current_device();                       // throws LDSP_EHIP when no GPU is present
 hipStream_t library_stream(int device);     // per-device non-blocking stream for host-memory calls
 

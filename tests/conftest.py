@@ -8,7 +8,7 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PKG = os.path.join(REPO, "python-liquiddsp_amd")
+PKG = os.environ.get("LDSP_PKG_DIR") or os.path.join(REPO, "python-liquiddsp_amd")
 for p in (REPO, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
