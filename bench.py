@@ -461,6 +461,17 @@ def components(L, device, reps=5):
                                "nco_GBs": round(16 * n / t["k_nco_mix"] / 1e6, 1),
                                "fir_GBs": round(16 * n / t[fk] / 1e6, 1),
                                "Msamples_s": round(n / (t["k_nco_mix"] + t[fk]) / 1e3, 1)}
+    # the same chain fused (liquiddsp.mix_down_filter: the mix happens in the FIR's
+    # window loads): 16 B per sample of HBM traffic instead of 32
+    nco_f = L.NCO("nco")
+    nco_f.freq = float(2 * np.pi * 0.05)
+    f3 = L.ComplexFIRFilter(kaiser(255, 0.05, 60.0))
+    t = timed(lambda: L.mix_down_filter(nco_f, f3, xs))
+    (fk, ms), = t.items()
+    out["nco_fir255_256Mi_fused"] = {"kernel": fk, "ms": round(ms, 4), "Msamples_s": round(n / ms / 1e3, 1),
+                                     "alg_GBs": round(16 * n / ms / 1e6, 1),
+                                     "hbm_frac": round(16 * n / ms / 1e6 / HBM_PEAK_GBS, 4),
+                                     "roof_ms": round(16 * n / HBM_PEAK_GBS / 1e6, 4)}
     del xs
     out["host_buffers"] = host_path(L, device)
     out["channels_per_gpu"] = multi_channel(L, device)

@@ -145,6 +145,17 @@ int ldsp_nco_get_state(ldsp_nco_t q, uint32_t *theta, uint32_t *dtheta);
 int ldsp_nco_set_state(ldsp_nco_t q, uint32_t theta, uint32_t dtheta);
 int ldsp_nco_mix(ldsp_nco_t q, const void *x, size_t n, void *y, int down, int mem, void *stream);
 
+/* NCO mix fused into a complex FIR: y = fir(nco.mix_down(x)) (down = 1) or
+ * fir(nco.mix_up(x)), the chain of BASELINE config 3 (reference src/nco.hpp:74-80
+ * NCO::mix_down, then src/firfilter.hpp:29-35 execute_block).  Advances the NCO
+ * phase by n * dtheta and the filter's history exactly as ldsp_nco_mix followed
+ * by ldsp_firfilt_execute would, with the same output bits; on the filter's
+ * overlap-save path (fast mode, table NCO) the mixed samples are formed as the
+ * filter loads x and never reach memory (16 B per sample instead of 32).  The
+ * filter must be complex (firfilt_crcf); both objects on the buffer's device. */
+int ldsp_nco_mix_firfilt(ldsp_nco_t nco, ldsp_firfilt_t fir, const void *x, size_t n, void *y, int down, int mem,
+                         void *stream);
+
 /* ------------------------------------------------------------------------
  * IIR filter: iirfilt_rrrf (cplx=0) / iirfilt_crcf (cplx=1).  Replaces
  * ComplexIIRFilter / RealIIRFilter (src/iirfilter.hpp:243-356,

@@ -149,6 +149,7 @@ struct FirObj {
     int device = -1;
     DevBuf taps_pad, taps_rev, hist[2];
     DevBuf fft_H, fft_tw;             // overlap-save spectrum (for fft_scale) and twiddles
+    DevBuf mixbuf;                    // ldsp_nco_mix_firfilt off the fused path: the mixed samples
     float fft_scale = 0.0f;
     bool fft_ready = false;
     int cur = 0;
@@ -978,6 +979,28 @@ int ldsp_firfilt_freqresponse(ldsp_firfilt_t q, float f, float* re, float* im)
     });
 }
 
+// One filter call on device buffers, in stream order after the object's
+// previous call; `fuse` applies an NCO mix to the samples as the overlap-save
+// kernel loads them (only on that path: the caller checks fir_can_fuse).
+static void fir_dispatch(ldsp_firfilt_s* q, const void* dx, size_t n, void* dy, hipStream_t s, const k::NcoFuse* fuse)
+{
+    const int L = (int)q->h.size();
+    void* hin = q->hist[q->cur].p;
+    void* hout = q->hist[1 - q->cur].p;
+    if (L <= 1 && n == 0) return;
+    if (q->mode == LDSP_MODE_EXACT)
+        k::fir_exact(q->cplx, dx, hin, hout, n, q->taps_rev.as<float>(), L, q->scale, dy, s);
+    else if (q->use_fft() && n > 0) {
+        if (!q->fft_ready || q->fft_scale != q->scale) {
+            LDSP_HIP(hipStreamSynchronize(s));   // tables may be in use by queued work
+            q->prepare_fft();
+        }
+        k::fir_fft(dx, hin, hout, n, L, q->fft_P(), q->fft_H.p, q->fft_tw.p, dy, s, fuse);
+    } else
+        k::fir_fast(q->cplx, dx, hin, hout, n, q->taps_pad.as<float>(), L, q->scale, dy, s);
+    if (L > 1) q->cur = 1 - q->cur;
+}
+
 int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
     return guard([&] {
@@ -991,22 +1014,7 @@ int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int
         const size_t bytes = n * q->esz();
         const void* dx = q->stg.dev_in(e, x, bytes);
         void* dy = q->stg.dev_out(e, y, bytes);
-        const int L = (int)q->h.size();
-        void* hin = q->hist[q->cur].p;
-        void* hout = q->hist[1 - q->cur].p;
-        if (L > 1 || n > 0) {
-            if (q->mode == LDSP_MODE_EXACT)
-                k::fir_exact(q->cplx, dx, hin, hout, n, q->taps_rev.as<float>(), L, q->scale, dy, e.stream);
-            else if (q->use_fft() && n > 0) {
-                if (!q->fft_ready || q->fft_scale != q->scale) {
-                    LDSP_HIP(hipStreamSynchronize(e.stream));   // tables may be in use by queued work
-                    q->prepare_fft();
-                }
-                k::fir_fft(dx, hin, hout, n, L, q->fft_P(), q->fft_H.p, q->fft_tw.p, dy, e.stream);
-            } else
-                k::fir_fast(q->cplx, dx, hin, hout, n, q->taps_pad.as<float>(), L, q->scale, dy, e.stream);
-            if (L > 1) q->cur = 1 - q->cur;
-        }
+        fir_dispatch(q, dx, n, dy, e.stream, nullptr);
         q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, bytes);
@@ -1139,6 +1147,11 @@ int ldsp_resamp_execute(ldsp_resamp_t q, const void* x, size_t n, void* y, size_
             while (KB > 1 && (size_t)span_for(KB) * q->esz() > 48 * 1024) KB >>= 1;
             p.KB = KB;
             p.span_max = span_for(KB);
+            const int tkb = k::resamp_tile_outputs(q->step, (int)q->sub_len, (int)q->npfb, q->cplx, q->real_taps);
+            if (tkb > 0) {
+                p.KB = tkb;
+                p.tile = 1;
+            }
             k::resamp(q->cplx, q->real_taps, dx, q->hist[q->cur].p, q->hist[1 - q->cur].p, n, q->dsub.as<float>(), p, dy,
                       e.stream);
             if (q->sub_len > 1) q->cur = 1 - q->cur;
@@ -1233,6 +1246,43 @@ int ldsp_nco_mix(ldsp_nco_t q, const void* x, size_t n, void* y, int down, int m
         k::nco_mix(dx, dy, n, q->theta, q->dtheta, q->dtab.as<float>(), down != 0, q->type, e.stream);
         q->theta += (uint32_t)((uint64_t)n * q->dtheta);
         q->stg.finish(e, y, n * 8);
+    });
+}
+
+// NCO mix fused into the complex FIR (BASELINE config 3): y = fir(nco.mix(x)).
+int ldsp_nco_mix_firfilt(ldsp_nco_t nco, ldsp_firfilt_t q, const void* x, size_t n, void* y, int down, int mem,
+                         void* stream)
+{
+    return guard([&] {
+        NONNULL(nco);
+        NONNULL(q);
+        LDSP_REQUIRE(q->cplx, "nco_mix_firfilt: the filter must be complex (firfilt_crcf / ComplexFIRFilter)");
+        LDSP_REQUIRE(n == 0 || (x && y), "nco_mix_firfilt: NULL buffer");
+        const BufDevice bd(mem, x);
+        q->ensure_device();
+        nco->ensure_device();
+        LDSP_REQUIRE(nco->device == q->device, "nco_mix_firfilt: the NCO and the filter live on different devices");
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream, bd);
+        q->ord.wait(e.stream);
+        const size_t bytes = n * 8;
+        const void* dx = q->stg.dev_in(e, x, bytes);
+        void* dy = q->stg.dev_out(e, y, bytes);
+        if (n > 0 && q->use_fft() && nco->type == 0) {
+            const k::NcoFuse f{nco->theta, nco->dtheta, down != 0, nco->dtab.as<float>()};
+            fir_dispatch(q, dx, n, dy, e.stream, &f);          // the mixed samples never reach HBM
+        } else if (n > 0) {
+            // other filter modes / the VCO: mix into scratch, then filter (same results)
+            void* mb = q->mixbuf.ensure(bytes, q->device);
+            k::nco_mix(dx, mb, n, nco->theta, nco->dtheta, nco->dtab.as<float>(), down != 0, nco->type, e.stream);
+            fir_dispatch(q, mb, n, dy, e.stream, nullptr);
+        } else {
+            fir_dispatch(q, dx, 0, dy, e.stream, nullptr);
+        }
+        nco->theta += (uint32_t)((uint64_t)n * nco->dtheta);
+        q->ord.mark(e.stream);
+        q->last = e.stream;
+        q->stg.finish(e, y, bytes);
     });
 }
 

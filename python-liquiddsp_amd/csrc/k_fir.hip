@@ -393,13 +393,132 @@ __global__ void __launch_bounds__(256) k_resamp_direct(const void* __restrict__ 
     y[k] = r;
 }
 
+// Tile variant (the default): a workgroup of kRsThreads computes p.KB
+// consecutive outputs.  Their input span [a, jhi] -- a = j(k0) - halo, moved
+// down to a 16-byte boundary -- is streamed into LDS with 16-byte loads, all of
+// a thread's loads issued before the first wait, so every HBM line is fetched
+// once by full-width coalesced loads; then each output runs its sub_len-tap
+// dot product from LDS in the restatement's order (bit-identical to
+// k_resamp_direct).  Branch taps live in LDS beside the span.
+constexpr int kRsThreads = 256;
+typedef float rs_f4 __attribute__((ext_vector_type(4)));
+
+template <bool CPLX, bool RT>
+__global__ void __launch_bounds__(kRsThreads) k_resamp_tile(const void* __restrict__ xv_, const void* __restrict__ hist_,
+                                                          void* __restrict__ hist_out_, long n,
+                                                          const float* __restrict__ sub, ResampPlan p, int tap_bytes,
+                                                          void* __restrict__ y_)
+{
+    using T = typename std::conditional<CPLX, float2, float>::type;
+    using TT = typename std::conditional<CPLX && !RT, float2, float>::type;   // tap type
+    constexpr int V = 16 / (int)sizeof(T);                                   // samples per 16-byte load
+    const T* __restrict__ x = (const T*)xv_;
+    const T* __restrict__ hist = (const T*)hist_;
+    T* y = (T*)y_;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    TT* taps = reinterpret_cast<TT*>(smem);                     // [npfb][sub_len]
+    T* win = reinterpret_cast<T*>(smem + tap_bytes);            // the span, 16-byte aligned
+    const int tid = threadIdx.x;
+    const int halo = p.sub_len - 1;
+    if (blockIdx.x == 0) {
+        T* hist_out = (T*)hist_out_;
+        for (int j = tid; j < halo; j += kRsThreads) {
+            const long gi = n - halo + j;
+            hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+        }
+    }
+    const TT* subT = (const TT*)sub;
+    for (int i = tid; i < p.npfb * p.sub_len; i += kRsThreads) taps[i] = subT[i];
+    const long k0 = (long)blockIdx.x * p.KB;
+    const long k1 = min((long)p.K, k0 + p.KB);
+    const long jlo = resamp_j(p.P0, k0, p.step) - halo;
+    const long jhi = resamp_j(p.P0, k1 - 1, p.step);          // < n
+    const long mis = (long)(((uintptr_t)x / sizeof(T)) & (V - 1));   // x's misalignment in samples
+    const long a = ((jlo + mis) & ~(long)(V - 1)) - mis;      // x + a is 16-byte aligned
+    const int cnt = (int)(jhi - a + 1);
+    if (a >= 0) {
+        const int nvec = (int)min((long)(cnt / V), (n - a) / V);
+        const rs_f4* __restrict__ xv = reinterpret_cast<const rs_f4*>(x + a);
+        rs_f4* wv = reinterpret_cast<rs_f4*>(win);
+        constexpr int U = 8;
+        for (int v0 = tid; v0 < nvec; v0 += kRsThreads * U) {
+            rs_f4 r[U];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (v0 + u * kRsThreads < nvec) r[u] = __builtin_nontemporal_load(xv + v0 + u * kRsThreads);
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (v0 + u * kRsThreads < nvec) wv[v0 + u * kRsThreads] = r[u];
+        }
+        for (int e = nvec * V + tid; e < cnt; e += kRsThreads) win[e] = x[a + e];
+    } else {                                                  // the call's first outputs: history ++ x
+        for (int e = tid; e < cnt; e += kRsThreads) {
+            const long gi = a + e;
+            T v{};
+            if (gi >= 0) v = x[gi];
+            else if (gi >= -halo) v = hist[gi + halo];
+            win[e] = v;
+        }
+    }
+    __syncthreads();
+    const long k = k0 + tid;
+    if (k >= k1) return;
+    const long j = resamp_j(p.P0, k, p.step);
+    const uint64_t ph = p.P0 + (uint64_t)k * p.step - ((uint64_t)j << 24);
+    const int b = (int)(ph >> p.bits_index);
+    const TT* hb = taps + (size_t)b * p.sub_len;
+    const T* xb = win + (j - halo - a);
+    T r{};
+    for (int i = 0; i < p.sub_len; i++) {
+        if constexpr (CPLX && RT) rs_mac_cr(r, hb[i], xb[i]);
+        else if constexpr (CPLX) rs_mac(r, hb[i], xb[i]);
+        else r = r + hb[i] * xb[i];
+    }
+    y[k] = r;
+}
+
 } // namespace
+
+int resamp_tile_outputs(uint32_t step, int sub_len, int npfb, bool cplx, bool real_taps)
+{
+    // outputs per workgroup: as many as the threads, halved until taps + span fit 48 KiB
+    const size_t elem = cplx ? 8 : 4;
+    const size_t tap = ((size_t)npfb * sub_len * ((cplx && !real_taps) ? 8 : 4) + 15) / 16 * 16;
+    int kb = kRsThreads;
+    auto bytes = [&](int q) { return tap + (((uint64_t)(q - 1) * step >> 24) + sub_len + 4) * elem; };
+    while (kb > 1 && bytes(kb) > 48 * 1024) kb >>= 1;
+    return bytes(kb) <= 64 * 1024 ? kb : 0;
+}
 
 void resamp(bool cplx, bool real_taps, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
             const ResampPlan& p, void* y, hipStream_t s)
 {
     const size_t elem = cplx ? 8 : 4;
     const size_t tap_lds = (size_t)p.npfb * p.sub_len * ((cplx && !real_taps) ? 8 : 4);
+    if (p.KB > 0 && p.tile && p.K > 0) {
+        const int tap_bytes = (int)((tap_lds + 15) / 16 * 16);
+        const size_t lds = (size_t)tap_bytes + (((uint64_t)(p.KB - 1) * p.step >> 24) + p.sub_len + 4) * elem;
+        const unsigned g = (unsigned)((p.K + p.KB - 1) / p.KB);
+        auto go = [&](const void* fn) {
+            LDSP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        };
+        LDSP_PROF(s, "k_resamp");
+        if (cplx && real_taps) {
+            go((const void*)k_resamp_tile<true, true>);
+            hipLaunchKernelGGL((k_resamp_tile<true, true>), dim3(g), dim3(kRsThreads), lds, s, x, hist, hist_out,
+                               (long)n, sub, p, tap_bytes, y);
+        } else if (cplx) {
+            go((const void*)k_resamp_tile<true, false>);
+            hipLaunchKernelGGL((k_resamp_tile<true, false>), dim3(g), dim3(kRsThreads), lds, s, x, hist, hist_out,
+                               (long)n, sub, p, tap_bytes, y);
+        } else {
+            go((const void*)k_resamp_tile<false, false>);
+            hipLaunchKernelGGL((k_resamp_tile<false, false>), dim3(g), dim3(kRsThreads), lds, s, x, hist, hist_out,
+                               (long)n, sub, p, tap_bytes, y);
+        }
+        LDSP_HIP(hipGetLastError());
+        return;
+    }
     if (tap_lds <= 64 * 1024 && p.K > 0) {
         const unsigned g = (unsigned)((p.K + 255) / 256);
         LDSP_PROF(s, "k_resamp");

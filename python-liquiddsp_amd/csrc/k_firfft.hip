@@ -177,14 +177,44 @@ __device__ __forceinline__ void fft512(float2 (&v)[8], float2* d, const float2* 
 }
 
 
-template <int PPL>
+// Fused NCO mix (BASELINE config 3, NCO.mix_down -> ComplexFIRFilter): the raw
+// sample x[i] enters the filter as x[i] e^{-+j theta_i}, theta_i = theta0 + i
+// dtheta (mod 2^32), with the sine table and operation order of k_nco_mix
+// (nco_crcf_mix_block_{down,up}), so the filter sees bit for bit what the
+// separate mix kernel would have written.  The history holds mixed samples.
+struct Mix {
+    uint32_t theta0, dtheta;
+    int down;
+};
+__device__ __forceinline__ float2 nco_mix1(float2 v, long i, const Mix& mx, const float* tab)
+{
+    const uint32_t th = mx.theta0 + (uint32_t)i * mx.dtheta;
+    const uint32_t idx = ((th + (1u << 21)) >> 22) & 0x3ffu;
+    const float sn = tab[idx];
+    const float cs = tab[(idx + 256) & 0x3ffu];
+    float2 o;
+    if (mx.down) {   // x * conj(c + js): (a c - b (-s)) + j (a (-s) + b c)
+        o.x = v.x * cs - v.y * (-sn);
+        o.y = v.x * (-sn) + v.y * cs;
+    } else {         // x * (c + js)
+        o.x = v.x * cs - v.y * sn;
+        o.y = v.x * sn + v.y * cs;
+    }
+    return o;
+}
+
+template <int PPL, bool MIX>
 __device__ __forceinline__ void load_win(float2 (&v)[PPL], const float2* __restrict__ x,
-                                         const float2* __restrict__ hist, long n, int halo, long g0, int lane)
+                                         const float2* __restrict__ hist, long n, int halo, long g0, int lane,
+                                         const Mix& mx, const float* ntab)
 {
     if (g0 >= 0 && g0 + 64 * PPL <= n) {          // interior window: 32-bit lane offsets, no checks
         const float2* __restrict__ xb = x + g0;
 #pragma unroll
         for (int r = 0; r < PPL; r++) v[r] = xb[lane + 64 * r];
+        if (MIX)
+#pragma unroll
+            for (int r = 0; r < PPL; r++) v[r] = nco_mix1(v[r], g0 + lane + 64 * r, mx, ntab);
         return;
     }
 #pragma unroll
@@ -192,7 +222,10 @@ __device__ __forceinline__ void load_win(float2 (&v)[PPL], const float2* __restr
         const long gi = g0 + lane + 64 * r;
         float2 e = make_float2(0.0f, 0.0f);
         if (gi >= 0) {
-            if (gi < n) e = x[gi];
+            if (gi < n) {
+                e = x[gi];
+                if (MIX) e = nco_mix1(e, gi, mx, ntab);
+            }
         } else if (gi >= -halo) {
             e = hist[gi + halo];
         }
@@ -221,12 +254,14 @@ __device__ __forceinline__ void store_win(const float2 (&v)[PPL], float2* __rest
     }
 }
 
+template <bool MIX>
 __device__ __forceinline__ void write_hist(const float2* __restrict__ x, const float2* __restrict__ hist,
-                                           float2* __restrict__ hist_out, long n, int halo, int t, int nt)
+                                           float2* __restrict__ hist_out, long n, int halo, int t, int nt,
+                                           const Mix& mx, const float* ntab)
 {
     for (int j = t; j < halo; j += nt) {
         const long gi = n - halo + j;
-        hist_out[j] = gi >= 0 ? x[gi] : hist[gi + halo];
+        hist_out[j] = gi >= 0 ? (MIX ? nco_mix1(x[gi], gi, mx, ntab) : x[gi]) : hist[gi + halo];
     }
 }
 
@@ -235,31 +270,42 @@ constexpr int kVN = 512;
 constexpr int kVSlots = kVN + kVN / 8;
 constexpr int kVWaves = 4;
 
+template <bool MIX>
 __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __restrict__ x,
                                                              const float2* __restrict__ hist,
                                                              float2* __restrict__ hist_out, long n, int L, int P,
                                                              long nwin, long per, const float2* __restrict__ H,
-                                                             const float2* __restrict__ tw, float2* __restrict__ y)
+                                                             const float2* __restrict__ tw, float2* __restrict__ y,
+                                                             Mix mx, const float* __restrict__ table)
 {
     __shared__ float2 buf[kVWaves][kVSlots];
     __shared__ float2 ltw[kFft512Tw];
     __shared__ float2 lH[kVN];
+    __shared__ float ntab[MIX ? 1024 : 1];
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int M = kVN - P;
     const int halo = L - 1;
-    if (blockIdx.x == 0) write_hist(x, hist, hist_out, n, halo, t, 64 * kVWaves);
+    if (MIX)
+        for (int j = t; j < 1024; j += 64 * kVWaves) ntab[j] = table[j];
     for (int j = t; j < kFft512Tw; j += 64 * kVWaves) ltw[j] = tw[j];
     for (int j = t; j < kVN; j += 64 * kVWaves) lH[j] = H[j];
     __syncthreads();
+    if (blockIdx.x == 0) write_hist<MIX>(x, hist, hist_out, n, halo, t, 64 * kVWaves, mx, ntab);
     const long w0 = ((long)blockIdx.x * kVWaves + wave) * per;
     const long w1 = min(nwin, w0 + per);
     float2* d = buf[wave];
+    // the next window's loads are issued before this one's transforms (one
+    // window of HBM reads in flight per wave beside the compute)
+    float2 nx[8];
+    if (w0 < w1) load_win<8, MIX>(nx, x, hist, n, halo, w0 * M - P, lane, mx, ntab);
     for (long w = w0; w < w1; w++) {
         const long g0 = w * M - P;
         float2 v[8];
-        load_win<8>(v, x, hist, n, halo, g0, lane);
+#pragma unroll
+        for (int r = 0; r < 8; r++) v[r] = nx[r];
+        if (w + 1 < w1) load_win<8, MIX>(nx, x, hist, n, halo, g0 + M, lane, mx, ntab);
         fft512(v, d, ltw, lane);
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -277,22 +323,27 @@ __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __res
 constexpr int kWSlots = kWN_ + kWN_ / 16;
 constexpr int kWaves = 8;
 
+template <bool MIX>
 __global__ void __launch_bounds__(64 * kWaves) k_fir_fft1024(const float2* __restrict__ x,
                                                              const float2* __restrict__ hist,
                                                              float2* __restrict__ hist_out, long n, int L, int P,
                                                              long nwin, long per, const float2* __restrict__ H,
-                                                             const float2* __restrict__ tw, float2* __restrict__ y)
+                                                             const float2* __restrict__ tw, float2* __restrict__ y,
+                                                             Mix mx, const float* __restrict__ table)
 {
     __shared__ float2 buf[kWaves][kWSlots];
     __shared__ float2 ltw[kFft1024Tw];
+    __shared__ float ntab[MIX ? 1024 : 1];
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int M = kWN_ - P;
     const int halo = L - 1;
-    if (blockIdx.x == 0) write_hist(x, hist, hist_out, n, halo, t, 64 * kWaves);
+    if (MIX)
+        for (int j = t; j < 1024; j += 64 * kWaves) ntab[j] = table[j];
     for (int j = t; j < kFft1024Tw; j += 64 * kWaves) ltw[j] = tw[j];
     __syncthreads();
+    if (blockIdx.x == 0) write_hist<MIX>(x, hist, hist_out, n, halo, t, 64 * kWaves, mx, ntab);
     const long w0 = ((long)blockIdx.x * kWaves + wave) * per;
     const long w1 = min(nwin, w0 + per);
     float2* d = buf[wave];
@@ -300,7 +351,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_fir_fft1024(const float2* __res
         asm volatile("" ::: "memory");    // keep H reads inside the loop (register budget)
         const long g0 = w * M - P;
         float2 v[16];
-        load_win<16>(v, x, hist, n, halo, g0, lane);
+        load_win<16, MIX>(v, x, hist, n, halo, g0, lane, mx, ntab);
         fft1024(v, d, ltw, lane);
 #pragma unroll
         for (int s = 0; s < 16; s++) {
@@ -327,7 +378,7 @@ long resident_waves(const void* fn, int threads)
 int fir_fft_points(int P) { return P <= 128 ? kVN : kWN_; }
 
 void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, int P, const void* H, const void* tw,
-             void* y, hipStream_t s)
+             void* y, hipStream_t s, const NcoFuse* nco)
 {
     if (n == 0) return;
     const bool small = P <= 128;
@@ -337,22 +388,38 @@ void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, i
     static long slots512 = 0, slots1024 = 0;
     long& slots = small ? slots512 : slots1024;
     if (slots == 0)
-        slots = small ? resident_waves((const void*)k_fir_fft512, 64 * kVWaves)
-                      : resident_waves((const void*)k_fir_fft1024, 64 * kWaves);
+        slots = small ? resident_waves((const void*)k_fir_fft512<false>, 64 * kVWaves)
+                      : resident_waves((const void*)k_fir_fft1024<false>, 64 * kWaves);
     const int wpb = small ? kVWaves : kWaves;
     const long waves = std::min(nwin, slots);
     const long per = (nwin + waves - 1) / waves;       // contiguous windows per wave
     const long used = (nwin + per - 1) / per;
     const unsigned grid = (unsigned)((used + wpb - 1) / wpb);
-    LDSP_PROF(s, small ? "k_fir_fft512" : "k_fir_fft1024");
-    if (small)
-        hipLaunchKernelGGL(k_fir_fft512, dim3(grid), dim3(64 * kVWaves), 0, s, (const float2*)x,
-                           (const float2*)hist, (float2*)hist_out, (long)n, L, P, nwin, per, (const float2*)H,
-                           (const float2*)tw, (float2*)y);
-    else
-        hipLaunchKernelGGL(k_fir_fft1024, dim3(grid), dim3(64 * kWaves), 0, s, (const float2*)x,
-                           (const float2*)hist, (float2*)hist_out, (long)n, L, P, nwin, per, (const float2*)H,
-                           (const float2*)tw, (float2*)y);
+    Mix mx{0u, 0u, 0};
+    const float* tab = nullptr;
+    if (nco) {
+        mx = Mix{nco->theta0, nco->dtheta, nco->down ? 1 : 0};
+        tab = nco->table;
+    }
+    const float2 *xc = (const float2*)x, *hc = (const float2*)hist, *Hc = (const float2*)H, *tc = (const float2*)tw;
+    float2 *ho = (float2*)hist_out, *yc = (float2*)y;
+    if (nco) {
+        LDSP_PROF(s, small ? "k_fir_fft512_nco" : "k_fir_fft1024_nco");
+        if (small)
+            hipLaunchKernelGGL(k_fir_fft512<true>, dim3(grid), dim3(64 * kVWaves), 0, s, xc, hc, ho, (long)n, L, P,
+                               nwin, per, Hc, tc, yc, mx, tab);
+        else
+            hipLaunchKernelGGL(k_fir_fft1024<true>, dim3(grid), dim3(64 * kWaves), 0, s, xc, hc, ho, (long)n, L, P,
+                               nwin, per, Hc, tc, yc, mx, tab);
+    } else {
+        LDSP_PROF(s, small ? "k_fir_fft512" : "k_fir_fft1024");
+        if (small)
+            hipLaunchKernelGGL(k_fir_fft512<false>, dim3(grid), dim3(64 * kVWaves), 0, s, xc, hc, ho, (long)n, L, P,
+                               nwin, per, Hc, tc, yc, mx, tab);
+        else
+            hipLaunchKernelGGL(k_fir_fft1024<false>, dim3(grid), dim3(64 * kWaves), 0, s, xc, hc, ho, (long)n, L, P,
+                               nwin, per, Hc, tc, yc, mx, tab);
+    }
     LDSP_HIP(hipGetLastError());
 }
 

@@ -15,8 +15,9 @@
 // keeps a residual), so chunk-parallel speculation cannot be verified by state
 // equality as for the AGC; instead:
 //   k_pll_cand : every chunk of 256 samples runs W samples early from an
-//                extrapolated state and records, per sample, its phase and the
-//                kick / output differences of the neighbouring indices i-1, i+1;
+//                extrapolated state and records, per sample, its phase, kicks
+//                and output (the neighbouring index a repair needs is evaluated
+//                later, by k_pll_entries, and only at the entries);
 //   k_pll_walk : one workgroup walks 1024-sample blocks in order with the exact offset
 //                of the true trajectory from the candidate; a 64-lane ballot
 //                finds the next sample whose true index differs, only that
@@ -120,13 +121,16 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
 
 // ------------------------------------------------------------------ candidates
 // Candidate chunks of kCand samples.  Per sample the candidate kernel writes
-// its output to y and a record (AoS, 2 x uint4 = 32 B):
-//   R0 = (w = theta + 2^21, dk1(i-1), dk2(i-1), dk1(i+1)),  R1 = (dk2(i+1), out(i-1), out(i+1), out(i))
-// (dk = kick at table index i -+ 1 minus kick at the candidate's index i),
+// its output to y and a record (uint4 = 16 B)
+//   R = (w = theta + 2^21, k1, k2, out)      (the loop's kicks and output at index i = w >> 22)
 // and per chunk its start / end state and its entry count (see the walker).
+// The kicks and output at the neighbouring index i -+ 1 -- what a repair
+// substitutes -- are evaluated by k_pll_entries for the entries only (~1/4 of
+// the samples, in parallel): the candidate's serial loop does one phase-detector
+// evaluation per sample, not three.
 constexpr int kBlkE = 512;        // walker block: entries
 struct CandBuf {
-    uint4* rec;           // [npad][2]
+    uint4* rec;           // [npad] (w, k1, k2, out)
     uint32_t* cs;         // [nchc][2] candidate state at chunk start
     uint32_t* ce;         // [nchc][2] candidate state at chunk end
     uint32_t* cnt;        // [nchc] entries per chunk
@@ -185,11 +189,11 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
             }
         }
         // REC: the group's records and outputs are kept in registers and stored
-        // back to back after it, so each lane's 256 B of records and 32 B of
+        // back to back after it, so each lane's 128 B of records and 32 B of
         // outputs reach L2 as whole lines (stored one sample at a time, ~1 us
         // apart, the partly written lines were evicted by the streaming kernels
-        // beside this one and reached HBM 3-4 times over).
-        uint4 r0[kB], r1[kB];
+        // beside this one and reached HBM several times over).
+        uint4 r0[kB];
         float yo[kB];
 #pragma unroll
         for (int j = 0; j < kB; j++) {
@@ -199,11 +203,7 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
                 if (REC) {
                     const long s = i + j;
                     const uint32_t w = theta + (1u << 21);
-                    const Kick km = pll_eval(tab, (ic - 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
-                    const Kick kp = pll_eval(tab, (ic + 1) & 0x3ffu, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
-                    r0[j] = make_uint4(w, km.k1 - kc.k1, km.k2 - kc.k2, kp.k1 - kc.k1);
-                    r1[j] = make_uint4(kp.k2 - kc.k2, __float_as_uint(km.out), __float_as_uint(kp.out),
-                                       __float_as_uint(kc.out));
+                    r0[j] = make_uint4(w, kc.k1, kc.k2, __float_as_uint(kc.out));
                     yo[j] = kc.out;
                     nent += (risky(w, cb.B) || s == a || s == b - 1) ? 1u : 0u;
                 }
@@ -214,18 +214,14 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
         if (REC) {
             if (i + kB <= b) {
 #pragma unroll
-                for (int j = 0; j < kB; j++) {
-                    cb.rec[2 * (i + j)] = r0[j];
-                    cb.rec[2 * (i + j) + 1] = r1[j];
-                }
+                for (int j = 0; j < kB; j++) cb.rec[i + j] = r0[j];
 #pragma unroll
                 for (int j = 0; j < kB; j++) y[i + j] = yo[j];
             } else {
 #pragma unroll
                 for (int j = 0; j < kB; j++)
                     if (i + j < b) {
-                        cb.rec[2 * (i + j)] = r0[j];
-                        cb.rec[2 * (i + j) + 1] = r1[j];
+                        cb.rec[i + j] = r0[j];
                         y[i + j] = yo[j];
                     }
             }
@@ -398,22 +394,25 @@ __global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
 //        while |f| < 2^21 (up if u >= 2^21, else down); the repair was right iff
 //        x_post - L' <= span (see below).
 // The tail of the last walker block is padded with W = ~0 (never an event).
-__global__ void __launch_bounds__(256) k_pll_entries(CandBuf cb, long n)
+__global__ void __launch_bounds__(256) k_pll_entries(PllIn in, const AmpState* st, CandBuf cb, long n)
 {
     LDSP_LATENCY_CRITICAL();
+    __shared__ float tab[1024];
+    for (int i = threadIdx.x; i < 1024; i += 256) tab[i] = in.table[i];
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const long k = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= cb.nchc) return;
+    const float alpha = st->alpha, beta = st->beta;
     const long b0 = k * kCand;
     const int nv = (int)min((long)kCand, n - b0);
-    uint4 R0[4], R1[4];
+    uint4 R0[4];
     unsigned long long M[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int i = r * 64 + lane;
         const long sg = b0 + min(i, nv - 1);
-        R0[r] = cb.rec[2 * sg];
-        R1[r] = cb.rec[2 * sg + 1];
+        R0[r] = cb.rec[sg];
         M[r] = __builtin_amdgcn_ballot_w64(i < nv && (risky(R0[r].x, cb.B) || i == 0 || i == nv - 1));
     }
     const uint32_t pth = cb.pth[k], pd = cb.pd[k];
@@ -440,8 +439,12 @@ __global__ void __launch_bounds__(256) k_pll_entries(CandBuf cb, long n)
             hi = min(hi, B);
         }
         const bool up = u >= (1u << 21);
-        const uint32_t dk1 = up ? R0[r].w : R0[r].y, dk2 = up ? R1[r].x : R0[r].z;
-        const uint32_t out = up ? R1[r].z : R1[r].y;
+        // the loop at the neighbouring table index (one cell up or down) minus the candidate's
+        const uint32_t ic = w >> 22;
+        const Kick kn = pll_eval(tab, (up ? ic + 1 : ic - 1) & 0x3ffu, in.x0[s], *x1_ptr(in, s), alpha, beta,
+                                 in.mod_index, in.costas);
+        const uint32_t dk1 = kn.k1 - R0[r].y, dk2 = kn.k2 - R0[r].z;
+        const uint32_t out = __float_as_uint(kn.out);
         // A repair here is right iff f_pre (the offset before it) lies in the
         // intersection of: the presumed one-cell crossing, [-B, B] if the left gap
         // is non-empty, and [-B - dk2, B - dk2] (f_post within B) if the right one
@@ -575,12 +578,12 @@ struct WState {
 
 // Generic walk of every sample in [sa, sb]: 64 consecutive samples per step
 // (records, offset model and loop inputs loaded one step ahead), each repair
-// taken from the record when the true index is one cell away and evaluated in
-// full (table in LDS) otherwise, its output written to y, the offsets of the
-// later lanes updated in place.  Used where the sparse walk cannot prove a gap
+// evaluated in full at the true index (table in LDS) against the candidate's
+// recorded kicks, its output written to y, the offsets of the later lanes
+// updated in place.  Used where the sparse walk cannot prove a gap
 // clean, and for every lane-block in the LDSP_DEBUG_PLL=2 check.
 struct FbGroup {
-    uint4 r0, r1;
+    uint4 r0;             // candidate record (w, k1, k2, out)
     uint32_t A;
     float2 u0, u1;
 };
@@ -588,8 +591,7 @@ __device__ __forceinline__ FbGroup fb_load(long base, long sb, const CandBuf& cb
 {
     FbGroup q;
     const long s = min(base + lane, sb);
-    q.r0 = cb.rec[2 * s];
-    q.r1 = cb.rec[2 * s + 1];
+    q.r0 = cb.rec[s];
     const long k = s / kCand;
     q.A = cb.pth[k] + (uint32_t)s * cb.pd[k];
     q.u0 = fc.x0[s];
@@ -612,28 +614,18 @@ __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_
         while (mask != 0) {
             const int j = __builtin_ctzll(mask);
             const uint32_t vj = rl(v, j);
-            uint32_t dk1, dk2, out;
-            if (vj - 0x400000u < 0x400000u) {                // one cell up
-                dk1 = rl(q.r0.w, j);
-                dk2 = rl(q.r1.x, j);
-                out = rl(q.r1.z, j);
-            } else if (vj >= 0xffc00000u) {                  // one cell down
-                dk1 = rl(q.r0.y, j);
-                dk2 = rl(q.r0.z, j);
-                out = rl(q.r1.y, j);
-            } else {                                         // further: the loop step in full
-                const uint32_t ic = rl(q.r0.x, j) >> 22;
-                const float2 u0 = make_float2(__uint_as_float(rl(__float_as_uint(q.u0.x), j)),
-                                              __uint_as_float(rl(__float_as_uint(q.u0.y), j)));
-                const float2 u1 = make_float2(__uint_as_float(rl(__float_as_uint(q.u1.x), j)),
-                                              __uint_as_float(rl(__float_as_uint(q.u1.y), j)));
-                const Kick kt = pll_eval(tab, (ic + (vj >> 22)) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index,
-                                         fc.costas);
-                const Kick kc = pll_eval(tab, ic, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas);
-                dk1 = rfl(kt.k1 - kc.k1);
-                dk2 = rfl(kt.k2 - kc.k2);
-                out = rfl(__float_as_uint(kt.out));
-            }
+            // the loop step at the true index (any number of cells from the
+            // candidate's), evaluated in full; the candidate's kicks from its record
+            const uint32_t ic = rl(q.r0.x, j) >> 22;
+            const float2 u0 = make_float2(__uint_as_float(rl(__float_as_uint(q.u0.x), j)),
+                                          __uint_as_float(rl(__float_as_uint(q.u0.y), j)));
+            const float2 u1 = make_float2(__uint_as_float(rl(__float_as_uint(q.u1.x), j)),
+                                          __uint_as_float(rl(__float_as_uint(q.u1.y), j)));
+            const Kick kt = pll_eval(tab, (ic + (vj >> 22)) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index,
+                                     fc.costas);
+            const uint32_t dk1 = rfl(kt.k1 - rl(q.r0.y, j));
+            const uint32_t dk2 = rfl(kt.k2 - rl(q.r0.z, j));
+            const uint32_t out = rfl(__float_as_uint(kt.out));
             const uint32_t rrel = (uint32_t)j + (uint32_t)(base - (long)S);
             if (lane == 0) y[base + j] = __uint_as_float(out);
             g.Kb += dk2 - rrel * dk1;
@@ -1088,7 +1080,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     for (int q = 0; q < kBlkE / 64; q++) {
                         const uint32_t sr = b.e[0][q * 64 + lane].z;
-                        if (q * 64 + lane < cnt) y[S + sr] = __uint_as_float(cb.rec[2 * ((long)S + sr) + 1].w);
+                        if (q * 64 + lane < cnt) y[S + sr] = __uint_as_float(cb.rec[(long)S + sr].w);
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     g.Kb = Kb0;
@@ -1192,7 +1184,7 @@ static PllLayout pll_layout(size_t n)
     L.nblkE = (long)((n + kBlkE - 1) / kBlkE);     // entries <= samples
     const size_t nc = (size_t)L.nchc;
     size_t o = 0;
-    L.rec = o;   o = al16(o + nc * kCand * 32);
+    L.rec = o;   o = al16(o + nc * kCand * 16);
     L.cs = o;    o = al16(o + nc * 8);
     L.ce = o;    o = al16(o + nc * 8);
     L.cnt = o;   o = al16(o + nc * 4);
@@ -1321,7 +1313,8 @@ void pll_front(const PllCall& c, hipStream_t s)
     LDSP_HIP(hipGetLastError());
     {
         LDSP_PROF(s, "k_pll_entries");
-        hipLaunchKernelGGL(k_pll_entries, dim3((unsigned)((cb.nchc + 3) / 4)), dim3(256), 0, s, cb, (long)c.n);
+        hipLaunchKernelGGL(k_pll_entries, dim3((unsigned)((cb.nchc + 3) / 4)), dim3(256), 0, s, pll_in(c),
+                           (const AmpState*)c.st, cb, (long)c.n);
     }
     LDSP_HIP(hipGetLastError());
 }

@@ -30,8 +30,16 @@ void fir_exact(bool cplx, const void* x, const void* hist, void* hist_out, size_
 constexpr int kFft512Tw = 7 * 8 + 7 * 64;
 constexpr int kFft1024Tw = 15 * 16 + 3 * 256;
 int fir_fft_points(int P);
+// Optional NCO mix fused into the window loads (table NCO, nco_crcf_mix_block_*):
+// sample i enters as x[i] e^{-+j theta}, theta = theta0 + i dtheta; hist then
+// holds mixed samples, like the filter's own history after a separate mix.
+struct NcoFuse {
+    uint32_t theta0, dtheta;
+    bool down;
+    const float* table;   // device sine table (1024)
+};
 void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, int P, const void* H, const void* tw,
-             void* y, hipStream_t s);
+             void* y, hipStream_t s, const NcoFuse* nco = nullptr);
 
 // ------------------------------------------------------------------ resampler
 struct ResampPlan {
@@ -43,7 +51,10 @@ struct ResampPlan {
     size_t K;             // outputs of this call
     int KB;               // outputs per workgroup
     int span_max;         // LDS samples per workgroup
+    int tile = 0;         // 1: k_resamp_tile (span streamed into LDS with 16-byte loads), KB from resamp_tile_outputs
 };
+// Outputs per workgroup of the tile kernel (0: its LDS would not fit; use the others).
+int resamp_tile_outputs(uint32_t step, int sub_len, int npfb, bool cplx, bool real_taps);
 // sub: [npfb][sub_len] branch taps reversed (cccf: complex64 with imag 0; rrrf, crcf: float)
 void resamp(bool cplx, bool real_taps, const void* x, const void* hist, void* hist_out, size_t n, const float* sub,
             const ResampPlan& p, void* y, hipStream_t s);

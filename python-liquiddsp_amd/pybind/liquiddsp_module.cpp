@@ -990,6 +990,26 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("mix_up", [](NCO& n, const py::handle& x) { return n.mix(x, false); })
         .def("mix_down", [](NCO& n, const py::handle& x) { return n.mix(x, true); });
 
+    // ---- NCO mix fused into a ComplexFIRFilter (BASELINE config 3; opt-in, not in wrapper.cpp)
+    m.def(
+        "mix_down_filter",
+        [](NCO& nco, ComplexFIRFilter& fir, const py::handle& x) {
+            return run_same(x, true, true, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+                return ldsp_nco_mix_firfilt(nco.q, fir.q, xi, n, yo, 1, mem, s);
+            });
+        },
+        py::arg("nco"), py::arg("fir"), py::arg("x"),
+        "fir(nco.mix_down(x)) in one pass: same output bits and state updates as the two calls");
+    m.def(
+        "mix_up_filter",
+        [](NCO& nco, ComplexFIRFilter& fir, const py::handle& x) {
+            return run_same(x, true, true, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
+                return ldsp_nco_mix_firfilt(nco.q, fir.q, xi, n, yo, 0, mem, s);
+            });
+        },
+        py::arg("nco"), py::arg("fir"), py::arg("x"),
+        "fir(nco.mix_up(x)) in one pass: same output bits and state updates as the two calls");
+
     // ---- bytes_to_iq, Delay (wrapper.cpp:13, 25-28)
     m.def("bytes_to_iq", &bytes_to_iq, py::arg("byts"));
     py::class_<Delay>(m, "Delay")

@@ -1,0 +1,115 @@
+"""Fused and restructured kernels at the BASELINE sizes.
+
+  * NCO mix fused into the complex FIR (BASELINE config 3: NCO.mix_down ->
+    255-tap ComplexFIRFilter; reference src/nco.hpp:74-80 then
+    src/firfilter.hpp:29-35): liquiddsp.mix_down_filter / mix_up_filter give
+    the same bits as the two calls on the GPU (same call boundaries, so the same
+    overlap-save windows), advance both objects' state identically, and stay
+    within SURVEY 8(d)'s 1e-6 of the restatement.
+  * The tile resampler (span streamed into LDS) at BASELINE config 2 size:
+    bit-identical to the restatement on 64 Mi samples in one call.
+"""
+import numpy as np
+import pytest
+
+from conftest import cgauss, maxrel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ld():
+    import liquiddsp
+    assert liquiddsp.device_count() > 0
+    return liquiddsp
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint64 if a.dtype == np.complex64 else np.uint32)
+
+
+@pytest.mark.parametrize("L", [51, 127, 255])
+@pytest.mark.parametrize("down", [True, False])
+def test_mix_filter_equals_two_calls(ld, ora, rng, L, down):
+    h = ora.firdes_kaiser(L, 0.05, 60.0)
+    x = cgauss(rng, 200_003)
+    cuts = [0, 1, 700, 70_000, 70_001, len(x)]
+
+    def pair():
+        nco = ld.NCO("nco")
+        nco.freq = np.float32(2 * np.pi * 0.05)
+        nco.phase = np.float32(0.25)
+        return nco, ld.ComplexFIRFilter(h)
+
+    n1, f1 = pair()
+    n2, f2 = pair()
+    fused = ld.mix_down_filter if down else ld.mix_up_filter
+    y = np.concatenate([fused(n1, f1, x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = np.concatenate([f2(n2.mix_down(x[a:b]) if down else n2.mix_up(x[a:b])) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert np.array_equal(bits(y), bits(ref))
+    assert n1.state() == n2.state()
+    on = ora.NCO(0)
+    on.freq = np.float32(2 * np.pi * 0.05)
+    on.phase = np.float32(0.25)
+    oref = ora.FIRFilter(h, cplx=True)(on.mix_down(x) if down else on.mix_up(x))
+    assert maxrel(y, oref) <= 1e-6
+    # the filter's history holds mixed samples: an unfused call afterwards continues the same stream
+    x2 = cgauss(rng, 5000)
+    assert np.array_equal(bits(f1(n1.mix_down(x2) if down else n1.mix_up(x2))),
+                          bits(f2(n2.mix_down(x2) if down else n2.mix_up(x2))))
+
+
+@pytest.mark.parametrize("case", ["exact", "direct", "vco"])
+def test_mix_filter_unfused_paths(ld, ora, rng, case):
+    h = ora.firdes_kaiser(127, 0.05, 60.0)
+    x = cgauss(rng, 50_000)
+    ncos, firs = [], []
+    for _ in range(2):
+        nco = ld.NCO("vco" if case == "vco" else "nco")
+        nco.freq = np.float32(0.3)
+        f = ld.ComplexFIRFilter(h)
+        if case != "vco":
+            f.mode = case
+        ncos.append(nco)
+        firs.append(f)
+    y = np.concatenate([ld.mix_down_filter(ncos[0], firs[0], x[:1234]), ld.mix_down_filter(ncos[0], firs[0], x[1234:])])
+    ref = np.concatenate([firs[1](ncos[1].mix_down(x[:1234])), firs[1](ncos[1].mix_down(x[1234:]))])
+    assert np.array_equal(bits(y), bits(ref))
+    with pytest.raises(TypeError):
+        ld.mix_down_filter(ncos[0], ld.RealFIRFilter(h), x)
+
+
+def test_mix_filter_config3_device(ld, ora):
+    """BASELINE config 3 shape on device tensors (64 Mi here; the bench runs 256 Mi):
+    fused == unfused bit for bit over a ragged two-call stream."""
+    import torch
+    n = 64 << 20
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    xd = torch.complex(torch.randn(n, generator=g, device="cuda"), torch.randn(n, generator=g, device="cuda"))
+    h = ora.firdes_kaiser(255, 0.05, 60.0)
+    out = []
+    for fused in (True, False):
+        nco = ld.NCO("nco")
+        nco.freq = np.float32(2 * np.pi * 0.05)
+        f = ld.ComplexFIRFilter(h)
+        parts = [xd[:12_345_677], xd[12_345_677:]]
+        ys = [ld.mix_down_filter(nco, f, p) if fused else f(nco.mix_down(p)) for p in parts]
+        out.append(torch.cat(ys))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0].view(torch.float32), out[1].view(torch.float32))
+
+
+def test_resampler_config2_full_size(ld, ora):
+    """BASELINE config 2: ComplexResampler(48k/2M) on 64 Mi samples in one call."""
+    import torch
+    n = 64 << 20
+    g = torch.Generator(device="cuda")
+    g.manual_seed(2)
+    xd = torch.complex(torch.randn(n, generator=g, device="cuda"), torch.randn(n, generator=g, device="cuda"))
+    r = ld.ComplexResampler(rate=np.float32(48000 / 2000000), Fc=np.float32(48000 / 2000000))
+    y = r(xd).cpu().numpy()
+    ref = ora.Resampler(np.float32(48000 / 2000000), 20, np.float32(48000 / 2000000), 60.0, 13)(xd.cpu().numpy())
+    assert y.shape == ref.shape == (1610613,)
+    assert np.array_equal(bits(y), bits(ref))
