@@ -319,6 +319,15 @@ struct IirObj {
     DevBuf db, da, st32, st64, sc1, sc2, mats;
     DevBuf bmats, bsc1, bsc2, bsc3;   // blocked scan (D <= 8): matrices and scratch
     int bplan_G = 0;
+    // single-pass scan (k_iir_1p): look-back depth (0: the filter decays too
+    // slowly, use the blocked scan), tables, per-block aggregates and flags,
+    // the ticket counter, the call epoch, and the second state buffer (the
+    // kernel reads the call's start state from st64 and writes the end state
+    // into st64b; the two are swapped after the call)
+    int J1p = 0;
+    DevBuf p1mats, p1agg, p1flags, p1ticket, st64b;
+    long p1_nblk_cap = 0;
+    unsigned p1_epoch = 0;
     bool state_in64 = false;          // where the authoritative state lives
     int plan_C = 0;
     long plan_nch = 0;
@@ -363,6 +372,25 @@ struct IirObj {
             v[c] = 1.0;
             step_host(v, 0.0);
             for (int r = 0; r < D; r++) A[(size_t)r * D + c] = v[r];
+        }
+        // single-pass scan: smallest J with ||A^(kIir1pBlock J)||_inf < 2^-70
+        J1p = 0;
+        if (D > 0 && D <= k::kIirBlkMaxD) {
+            const std::vector<double> AB = matpow(A, (uint64_t)k::kIir1pBlock);
+            std::vector<double> P = AB;
+            for (int j = 1; j <= k::kIir1pJmax; j++) {
+                double nrm = 0;
+                for (int r = 0; r < D; r++) {
+                    double sum = 0;
+                    for (int q = 0; q < D; q++) sum += fabs(P[(size_t)r * D + q]);
+                    nrm = std::max(nrm, sum);
+                }
+                if (nrm < 8.5e-22) {
+                    J1p = j;
+                    break;
+                }
+                P = matmul(P, AB);
+            }
         }
         // decay length: smallest 2^k with ||A^(2^k)||_inf < 2^-70
         spec_W = 0;
@@ -414,6 +442,7 @@ struct IirObj {
         zero_now(st32.p, 0, sizeof(float) * 2 * std::max(fsz(), 1));
         st64.ensure(sizeof(double) * 2 * std::max(D, 1), dev);
         zero_now(st64.p, 0, sizeof(double) * 2 * std::max(D, 1));
+        st64b.ensure(sizeof(double) * 2 * std::max(D, 1), dev);
         state_in64 = false;
         device = dev;
     }
@@ -501,6 +530,47 @@ struct IirObj {
         p.local = (double*)bsc1.ensure((size_t)nch * ncomp() * D * sizeof(double), device);
         p.blocal = (double*)bsc2.ensure((size_t)nblk * ncomp() * D * sizeof(double), device);
         p.bstart = (double*)bsc3.ensure((size_t)nblk * ncomp() * D * sizeof(double), device);
+        return p;
+    }
+    k::Iir1pPlan one_pass_plan(size_t n)
+    {
+        const size_t DD = (size_t)D * D;
+        if (!p1mats.p) {
+            std::vector<double> all;
+            const std::vector<double> A32 = matpow(A, 32);
+            std::vector<double> M = matpow(A, 0);
+            for (int j = 0; j < 256; j++) {           // A^{32 j}
+                all.insert(all.end(), M.begin(), M.end());
+                M = matmul(M, A32);
+            }
+            const std::vector<double> AB = matpow(A, (uint64_t)k::kIir1pBlock);
+            M = matpow(A, 0);
+            for (int j = 0; j < J1p; j++) {           // A^{kIir1pBlock j}
+                all.insert(all.end(), M.begin(), M.end());
+                M = matmul(M, AB);
+            }
+            upload(p1mats, all, device);
+            p1ticket.ensure(64, device);
+            zero_now(p1ticket.p, 0, 64);
+        }
+        const long nblk = (long)((n + k::kIir1pBlock - 1) / k::kIir1pBlock);
+        if (nblk > p1_nblk_cap) {                     // flags start at 0 (< every epoch)
+            p1flags.ensure((size_t)nblk * 4, device);
+            zero_now(p1flags.p, 0, p1flags.cap);
+            p1_nblk_cap = (long)(p1flags.cap / 4);
+        }
+        k::Iir1pPlan p;
+        p.J = J1p;
+        p.AC = p1mats.as<double>();
+        p.AB = p.AC + 256 * DD;
+        p.agg = (double*)p1agg.ensure((size_t)nblk * ncomp() * D * sizeof(double), device);
+        p.flags = p1flags.as<unsigned>();
+        p.ticket = p1ticket.as<unsigned>();
+        if (++p1_epoch == 0) {                        // wrapped: restart the flags
+            zero_now(p1flags.p, 0, p1flags.cap);
+            p1_epoch = 1;
+        }
+        p.epoch = p1_epoch;
         return p;
     }
     k::IirScanPlan scan_plan(size_t n)
@@ -1456,6 +1526,16 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
             } else if (q->mode == LDSP_MODE_EXACT) {
                 q->state_to(false, e.stream);
                 k::iir_seq(q->cplx, d, dx, n, q->st32.as<float>(), dy, e.stream);
+            } else if (q->J1p > 0 && LDSP_KNOB("LDSP_IIR_1P", 0)) {
+                // single pass (tuning builds only: measured 2.75 ms against 0.88 ms for the
+                // blocked scan at 64 Mi): reads st64 (the call's
+                // start), writes st64b (its end); then swap
+                q->state_to(true, e.stream);
+                const k::Iir1pPlan p = q->one_pass_plan(n);
+                k::iir_1p(q->cplx, d, q->b.data(), q->a.data(), dx, n, q->st64.as<double>(), q->st64b.as<double>(), p,
+                          dy, e.stream);
+                std::swap(q->st64.p, q->st64b.p);
+                std::swap(q->st64.cap, q->st64b.cap);
             } else if (q->D <= k::kIirBlkMaxD && !LDSP_KNOB("LDSP_IIR_OLDSCAN", 0)) {
                 q->state_to(true, e.stream);
                 const k::IirBlkPlan p = q->blk_plan(n);

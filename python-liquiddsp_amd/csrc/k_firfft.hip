@@ -186,12 +186,13 @@ struct Mix {
     uint32_t theta0, dtheta;
     int down;
 };
-__device__ __forceinline__ float2 nco_mix1(float2 v, long i, const Mix& mx, const float* tab)
+// tab: (sin, cos) pairs of the NCO table, tab[i] = (sintab[i], sintab[(i + 256) & 1023])
+__device__ __forceinline__ float2 nco_mix1(float2 v, long i, const Mix& mx, const float2* tab)
 {
     const uint32_t th = mx.theta0 + (uint32_t)i * mx.dtheta;
     const uint32_t idx = ((th + (1u << 21)) >> 22) & 0x3ffu;
-    const float sn = tab[idx];
-    const float cs = tab[(idx + 256) & 0x3ffu];
+    const float2 sc = tab[idx];
+    const float sn = sc.x, cs = sc.y;
     float2 o;
     if (mx.down) {   // x * conj(c + js): (a c - b (-s)) + j (a (-s) + b c)
         o.x = v.x * cs - v.y * (-sn);
@@ -206,7 +207,7 @@ __device__ __forceinline__ float2 nco_mix1(float2 v, long i, const Mix& mx, cons
 template <int PPL, bool MIX>
 __device__ __forceinline__ void load_win(float2 (&v)[PPL], const float2* __restrict__ x,
                                          const float2* __restrict__ hist, long n, int halo, long g0, int lane,
-                                         const Mix& mx, const float* ntab)
+                                         const Mix& mx, const float2* ntab)
 {
     if (g0 >= 0 && g0 + 64 * PPL <= n) {          // interior window: 32-bit lane offsets, no checks
         const float2* __restrict__ xb = x + g0;
@@ -257,7 +258,7 @@ __device__ __forceinline__ void store_win(const float2 (&v)[PPL], float2* __rest
 template <bool MIX>
 __device__ __forceinline__ void write_hist(const float2* __restrict__ x, const float2* __restrict__ hist,
                                            float2* __restrict__ hist_out, long n, int halo, int t, int nt,
-                                           const Mix& mx, const float* ntab)
+                                           const Mix& mx, const float2* ntab)
 {
     for (int j = t; j < halo; j += nt) {
         const long gi = n - halo + j;
@@ -266,11 +267,13 @@ __device__ __forceinline__ void write_hist(const float2* __restrict__ x, const f
 }
 
 // 512-point windows: 8 points per lane, 4 waves per workgroup; tables in LDS.
+// PREF: the next window's loads are issued before this one's transforms (one
+// window of HBM reads in flight per wave beside the compute; costs registers).
 constexpr int kVN = 512;
 constexpr int kVSlots = kVN + kVN / 8;
 constexpr int kVWaves = 4;
 
-template <bool MIX>
+template <bool MIX, bool PREF>
 __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __restrict__ x,
                                                              const float2* __restrict__ hist,
                                                              float2* __restrict__ hist_out, long n, int L, int P,
@@ -281,14 +284,14 @@ __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __res
     __shared__ float2 buf[kVWaves][kVSlots];
     __shared__ float2 ltw[kFft512Tw];
     __shared__ float2 lH[kVN];
-    __shared__ float ntab[MIX ? 1024 : 1];
+    __shared__ float2 ntab[MIX ? 1024 : 1];
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int M = kVN - P;
     const int halo = L - 1;
     if (MIX)
-        for (int j = t; j < 1024; j += 64 * kVWaves) ntab[j] = table[j];
+        for (int j = t; j < 1024; j += 64 * kVWaves) ntab[j] = make_float2(table[j], table[(j + 256) & 1023]);
     for (int j = t; j < kFft512Tw; j += 64 * kVWaves) ltw[j] = tw[j];
     for (int j = t; j < kVN; j += 64 * kVWaves) lH[j] = H[j];
     __syncthreads();
@@ -296,16 +299,18 @@ __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __res
     const long w0 = ((long)blockIdx.x * kVWaves + wave) * per;
     const long w1 = min(nwin, w0 + per);
     float2* d = buf[wave];
-    // the next window's loads are issued before this one's transforms (one
-    // window of HBM reads in flight per wave beside the compute)
     float2 nx[8];
-    if (w0 < w1) load_win<8, MIX>(nx, x, hist, n, halo, w0 * M - P, lane, mx, ntab);
+    if (PREF && w0 < w1) load_win<8, MIX>(nx, x, hist, n, halo, w0 * M - P, lane, mx, ntab);
     for (long w = w0; w < w1; w++) {
         const long g0 = w * M - P;
         float2 v[8];
+        if (PREF) {
 #pragma unroll
-        for (int r = 0; r < 8; r++) v[r] = nx[r];
-        if (w + 1 < w1) load_win<8, MIX>(nx, x, hist, n, halo, g0 + M, lane, mx, ntab);
+            for (int r = 0; r < 8; r++) v[r] = nx[r];
+            if (w + 1 < w1) load_win<8, MIX>(nx, x, hist, n, halo, g0 + M, lane, mx, ntab);
+        } else {
+            load_win<8, MIX>(v, x, hist, n, halo, g0, lane, mx, ntab);
+        }
         fft512(v, d, ltw, lane);
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -319,39 +324,47 @@ __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __res
     }
 }
 
-// 1024-point windows (P > 128): 16 points per lane, 8 waves per workgroup.
+// 1024-point windows (P > 128): 16 points per lane, WAVES waves per workgroup
+// (4: three workgroups share a CU at <= 168 registers; 8: one).
 constexpr int kWSlots = kWN_ + kWN_ / 16;
-constexpr int kWaves = 8;
 
-template <bool MIX>
-__global__ void __launch_bounds__(64 * kWaves) k_fir_fft1024(const float2* __restrict__ x,
-                                                             const float2* __restrict__ hist,
-                                                             float2* __restrict__ hist_out, long n, int L, int P,
-                                                             long nwin, long per, const float2* __restrict__ H,
-                                                             const float2* __restrict__ tw, float2* __restrict__ y,
-                                                             Mix mx, const float* __restrict__ table)
+template <bool MIX, int WAVES, bool PREF>
+__global__ void __launch_bounds__(64 * WAVES) k_fir_fft1024(const float2* __restrict__ x,
+                                                            const float2* __restrict__ hist,
+                                                            float2* __restrict__ hist_out, long n, int L, int P,
+                                                            long nwin, long per, const float2* __restrict__ H,
+                                                            const float2* __restrict__ tw, float2* __restrict__ y,
+                                                            Mix mx, const float* __restrict__ table)
 {
-    __shared__ float2 buf[kWaves][kWSlots];
+    __shared__ float2 buf[WAVES][kWSlots];
     __shared__ float2 ltw[kFft1024Tw];
-    __shared__ float ntab[MIX ? 1024 : 1];
+    __shared__ float2 ntab[MIX ? 1024 : 1];
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int M = kWN_ - P;
     const int halo = L - 1;
     if (MIX)
-        for (int j = t; j < 1024; j += 64 * kWaves) ntab[j] = table[j];
-    for (int j = t; j < kFft1024Tw; j += 64 * kWaves) ltw[j] = tw[j];
+        for (int j = t; j < 1024; j += 64 * WAVES) ntab[j] = make_float2(table[j], table[(j + 256) & 1023]);
+    for (int j = t; j < kFft1024Tw; j += 64 * WAVES) ltw[j] = tw[j];
     __syncthreads();
-    if (blockIdx.x == 0) write_hist<MIX>(x, hist, hist_out, n, halo, t, 64 * kWaves, mx, ntab);
-    const long w0 = ((long)blockIdx.x * kWaves + wave) * per;
+    if (blockIdx.x == 0) write_hist<MIX>(x, hist, hist_out, n, halo, t, 64 * WAVES, mx, ntab);
+    const long w0 = ((long)blockIdx.x * WAVES + wave) * per;
     const long w1 = min(nwin, w0 + per);
     float2* d = buf[wave];
+    float2 nx[16];
+    if (PREF && w0 < w1) load_win<16, MIX>(nx, x, hist, n, halo, w0 * M - P, lane, mx, ntab);
     for (long w = w0; w < w1; w++) {
         asm volatile("" ::: "memory");    // keep H reads inside the loop (register budget)
         const long g0 = w * M - P;
         float2 v[16];
-        load_win<16, MIX>(v, x, hist, n, halo, g0, lane, mx, ntab);
+        if (PREF) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) v[r] = nx[r];
+            if (w + 1 < w1) load_win<16, MIX>(nx, x, hist, n, halo, g0 + M, lane, mx, ntab);
+        } else {
+            load_win<16, MIX>(v, x, hist, n, halo, g0, lane, mx, ntab);
+        }
         fft1024(v, d, ltw, lane);
 #pragma unroll
         for (int s = 0; s < 16; s++) {
@@ -377,6 +390,46 @@ long resident_waves(const void* fn, int threads)
 
 int fir_fft_points(int P) { return P <= 128 ? kVN : kWN_; }
 
+// Kernel variant: (512: prefetch) x (1024: prefetch, 4 or 8 waves); the
+// defaults were measured on MI355X; tuning builds take
+// LDSP_FFT_VARIANT = bit 0 prefetch-512, bit 1 prefetch-1024, bit 2 1024 with 8 waves.
+constexpr int kFftVariantDefault = 2;   // 512 without prefetch (80 VGPRs, 6 waves / SIMD); 1024: 4 waves, prefetch
+
+template <bool MIX>
+static void fft_launch(bool small, int var, unsigned grid_of_waves_fn_unused, const float2* xc, const float2* hc,
+                       float2* ho, long n, int L, int P, long nwin, const float2* Hc, const float2* tc, float2* yc,
+                       const Mix& mx, const float* tab, hipStream_t s)
+{
+    (void)grid_of_waves_fn_unused;
+    auto run = [&](const void* fn, int wpb, auto launch) {
+        static long slots_cache[2][16] = {};
+        long& slots = slots_cache[MIX ? 1 : 0][(small ? 8 : 0) | (var & 7)];
+        if (slots == 0) slots = resident_waves(fn, 64 * wpb);
+        const long waves = std::min(nwin, slots);
+        const long per = (nwin + waves - 1) / waves;       // contiguous windows per wave
+        const long used = (nwin + per - 1) / per;
+        const unsigned grid = (unsigned)((used + wpb - 1) / wpb);
+        launch(grid, per);
+    };
+#define LDSP_FFT_LAUNCH(KERNEL, WPB)                                                                           \
+    run((const void*)KERNEL, WPB, [&](unsigned grid, long per) {                                                \
+        hipLaunchKernelGGL(KERNEL, dim3(grid), dim3(64 * (WPB)), 0, s, xc, hc, ho, n, L, P, nwin, per, Hc, tc, yc, \
+                           mx, tab);                                                                           \
+    })
+    if (small) {
+        if (var & 1) LDSP_FFT_LAUNCH((k_fir_fft512<MIX, true>), kVWaves);
+        else LDSP_FFT_LAUNCH((k_fir_fft512<MIX, false>), kVWaves);
+    } else {
+        switch (var & 6) {
+        case 0: LDSP_FFT_LAUNCH((k_fir_fft1024<MIX, 4, false>), 4); break;
+        case 2: LDSP_FFT_LAUNCH((k_fir_fft1024<MIX, 4, true>), 4); break;
+        case 4: LDSP_FFT_LAUNCH((k_fir_fft1024<MIX, 8, false>), 8); break;
+        default: LDSP_FFT_LAUNCH((k_fir_fft1024<MIX, 8, true>), 8); break;
+        }
+    }
+#undef LDSP_FFT_LAUNCH
+}
+
 void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, int P, const void* H, const void* tw,
              void* y, hipStream_t s, const NcoFuse* nco)
 {
@@ -385,16 +438,7 @@ void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, i
     const long N = small ? kVN : kWN_;
     const long M = N - P;
     const long nwin = (long)((n + M - 1) / M);
-    static long slots512 = 0, slots1024 = 0;
-    long& slots = small ? slots512 : slots1024;
-    if (slots == 0)
-        slots = small ? resident_waves((const void*)k_fir_fft512<false>, 64 * kVWaves)
-                      : resident_waves((const void*)k_fir_fft1024<false>, 64 * kWaves);
-    const int wpb = small ? kVWaves : kWaves;
-    const long waves = std::min(nwin, slots);
-    const long per = (nwin + waves - 1) / waves;       // contiguous windows per wave
-    const long used = (nwin + per - 1) / per;
-    const unsigned grid = (unsigned)((used + wpb - 1) / wpb);
+    static const int var = LDSP_KNOB("LDSP_FFT_VARIANT", kFftVariantDefault);
     Mix mx{0u, 0u, 0};
     const float* tab = nullptr;
     if (nco) {
@@ -405,20 +449,10 @@ void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, i
     float2 *ho = (float2*)hist_out, *yc = (float2*)y;
     if (nco) {
         LDSP_PROF(s, small ? "k_fir_fft512_nco" : "k_fir_fft1024_nco");
-        if (small)
-            hipLaunchKernelGGL(k_fir_fft512<true>, dim3(grid), dim3(64 * kVWaves), 0, s, xc, hc, ho, (long)n, L, P,
-                               nwin, per, Hc, tc, yc, mx, tab);
-        else
-            hipLaunchKernelGGL(k_fir_fft1024<true>, dim3(grid), dim3(64 * kWaves), 0, s, xc, hc, ho, (long)n, L, P,
-                               nwin, per, Hc, tc, yc, mx, tab);
+        fft_launch<true>(small, var, 0, xc, hc, ho, (long)n, L, P, nwin, Hc, tc, yc, mx, tab, s);
     } else {
         LDSP_PROF(s, small ? "k_fir_fft512" : "k_fir_fft1024");
-        if (small)
-            hipLaunchKernelGGL(k_fir_fft512<false>, dim3(grid), dim3(64 * kVWaves), 0, s, xc, hc, ho, (long)n, L, P,
-                               nwin, per, Hc, tc, yc, mx, tab);
-        else
-            hipLaunchKernelGGL(k_fir_fft1024<false>, dim3(grid), dim3(64 * kWaves), 0, s, xc, hc, ho, (long)n, L, P,
-                               nwin, per, Hc, tc, yc, mx, tab);
+        fft_launch<false>(small, var, 0, xc, hc, ho, (long)n, L, P, nwin, Hc, tc, yc, mx, tab, s);
     }
     LDSP_HIP(hipGetLastError());
 }

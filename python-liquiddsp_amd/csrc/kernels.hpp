@@ -111,6 +111,23 @@ struct IirBlkPlan {
 };
 void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n, double* state64,
              const IirBlkPlan& p, void* y, hipStream_t s);
+// Single-pass float64 scan (k_iir_1p, D <= 8): blocks of kIir1pBlock samples
+// (32 per thread), each block's start state from the J <= kIir1pJmax blocks
+// before it (decoupled look-back; valid when ||A^(kIir1pBlock J)|| < 2^-70).
+constexpr int kIir1pBlock = 8192;
+constexpr int kIir1pJmax = 8;
+struct Iir1pPlan {
+    int J;                // look-back depth (blocks)
+    const double* AC;     // A^{32 j}, j = 0..255                       [256][D*D]
+    const double* AB;     // A^{kIir1pBlock j}, j = 0..J-1              [J][D*D]
+    double* agg;          // [nblk][ncomp][D] each block's end state from a zero start
+    unsigned* flags;      // [nblk] = epoch once agg[b] is published (zeroed when allocated)
+    unsigned* ticket;     // dynamic block order (zero between calls)
+    unsigned epoch;       // per call, never 0
+};
+// st_in: the call's start state, st_out: its end state (distinct buffers)
+void iir_1p(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n,
+            const double* st_in, double* st_out, const Iir1pPlan& p, void* y, hipStream_t s);
 // Speculative exact evaluation for fast-decaying filters: chunks start from a
 // zero state W samples early; a verifier re-runs any chunk whose guessed
 // start state differs bit-wise from its predecessor's end state.

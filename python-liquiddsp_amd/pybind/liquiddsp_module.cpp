@@ -75,6 +75,13 @@ DevIn dev_in(const py::handle& x, bool cplx)
     t = t.attr("reshape")(-1).attr("contiguous")();
     DevIn d;
     d.device = t.attr("device");
+    // libldsp binds an object to the current HIP device on first use and
+    // launches there: a tensor on another device would hand it foreign pointers
+    const int tdev = d.device.attr("index").cast<int>();
+    const int cur = torch.attr("cuda").attr("current_device")().cast<int>();
+    if (tdev != cur)
+        throw py::value_error("input tensor is on cuda:" + std::to_string(tdev) + " but the current device is cuda:" +
+                              std::to_string(cur) + " (call under torch.cuda.device(" + std::to_string(tdev) + "))");
     d.ptr = reinterpret_cast<void*>(t.attr("data_ptr")().cast<uintptr_t>());
     d.n = t.attr("numel")().cast<size_t>();
     d.stream = reinterpret_cast<void*>(
