@@ -173,28 +173,58 @@ def host_info():
     return info
 
 
-def cpu_baseline(n_iq, seconds=10.0):
-    """Time the CPU restatement (oracle/, -O3, single thread) on a bounded sample."""
-    from oracle import oracle as O
-    rng = np.random.default_rng(4)
-    n = 1 << 22
+def _cpu_block(n, carrier, seed):
+    """synth_channel's AM signal, in numpy, for the CPU legs."""
+    rng = np.random.default_rng(seed)
     t = np.arange(n) / 2e6
     msg = (np.sin(2 * np.pi * 400 * t) + np.sin(2 * np.pi * 1000 * t) + np.sin(2 * np.pi * 2500 * t)) / 3
-    x = (0.1 * (1 + 0.5 * msg) * np.exp(1j * (2 * np.pi * 1200 * t))
-         + 0.00224 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))).astype(np.complex64)
-    radio = O.AMRadio()
+    return (0.1 * (1 + 0.5 * msg) * np.exp(1j * (2 * np.pi * carrier * t))
+            + 0.00224 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))).astype(np.complex64)
+
+
+def _cpu_run(radio, x, seconds):
+    """README-style 65,536-sample callbacks over x, repeated for about `seconds`;
+    returns (IQ samples done, elapsed s).  The oracle's ctypes calls release the GIL."""
     done = 0
     t0 = time.perf_counter()
     while True:
-        for i in range(0, n, 65536):        # README-style 65,536-sample callbacks
+        for i in range(0, len(x), 65536):
             radio(x[i:i + 65536])
-        done += n
+        done += len(x)
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": round(done / el / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"{done} IQ samples ({done // n} passes over a {n}-sample synthetic AM block) through the "
-                      f"oracle AMRadio chain in 65536-sample calls, single thread, {el:.1f} s"}
+            return done, el
+
+
+def cpu_baseline(n_iq, seconds=10.0, c5_seconds=5.0):
+    """Time the CPU restatement (oracle/, -O3) on bounded samples: one channel on
+    one thread (BASELINE config 4, the reported value) and SURVEY 8(d)'s C5 leg,
+    8 independent channels on min(8, nproc) threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    n = 1 << 22
+    x = _cpu_block(n, 1200.0, 4)
+    done, el = _cpu_run(O.AMRadio(), x, seconds)
+    res = {"value": round(done / el / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "sample": f"{done} IQ samples ({done // n} passes over a {n}-sample synthetic AM block) through the "
+                     f"oracle AMRadio chain in 65536-sample calls, single thread, {el:.1f} s"}
+    if c5_seconds > 0:
+        threads = max(1, min(8, os.cpu_count() or 1))
+        nc = 1 << 20
+        blocks = [_cpu_block(nc, CARRIERS[c], 10 + c) for c in range(8)]
+
+        def channel(c):
+            return _cpu_run(O.AMRadio(), blocks[c], c5_seconds)
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            outs = list(ex.map(channel, range(8)))
+        wall = time.perf_counter() - t0
+        tot = sum(d for d, _ in outs)
+        res["c5_channels"] = {
+            "value": round(tot / wall / 1e6, 3), "unit": "Msamples/s", "channels": 8, "cores": threads,
+            "sample": f"8 channels (carriers {CARRIERS}, seeds 10-17), {nc} IQ samples each, repeated "
+                      f"~{c5_seconds:.0f} s per channel in 65536-sample calls, {threads} threads, {wall:.1f} s wall"}
+    return res
 
 
 def main():

@@ -388,12 +388,19 @@ long resident_waves(const void* fn, int threads)
 
 } // namespace
 
-int fir_fft_points(int P) { return P <= 128 ? kVN : kWN_; }
-
 // Kernel variant: (512: prefetch) x (1024: prefetch, 4 or 8 waves); the
 // defaults were measured on MI355X; tuning builds take
-// LDSP_FFT_VARIANT = bit 0 prefetch-512, bit 1 prefetch-1024, bit 2 1024 with 8 waves.
+// LDSP_FFT_VARIANT = bit 0 prefetch-512, bit 1 prefetch-1024, bit 2 1024 with 8 waves,
+// bit 3 1024-point windows for short filters too.
 constexpr int kFftVariantDefault = 2;   // 512 without prefetch (80 VGPRs, 6 waves / SIMD); 1024: 4 waves, prefetch
+static int fft_variant()
+{
+    static const int var = LDSP_KNOB("LDSP_FFT_VARIANT", kFftVariantDefault);
+    return var;
+}
+static bool fft_small(int P) { return P <= 128 && !(fft_variant() & 8); }
+
+int fir_fft_points(int P) { return fft_small(P) ? kVN : kWN_; }
 
 template <bool MIX>
 static void fft_launch(bool small, int var, unsigned grid_of_waves_fn_unused, const float2* xc, const float2* hc,
@@ -434,11 +441,11 @@ void fir_fft(const void* x, const void* hist, void* hist_out, size_t n, int L, i
              void* y, hipStream_t s, const NcoFuse* nco)
 {
     if (n == 0) return;
-    const bool small = P <= 128;
+    const bool small = fft_small(P);
     const long N = small ? kVN : kWN_;
     const long M = N - P;
     const long nwin = (long)((n + M - 1) / M);
-    static const int var = LDSP_KNOB("LDSP_FFT_VARIANT", kFftVariantDefault);
+    const int var = fft_variant();
     Mix mx{0u, 0u, 0};
     const float* tab = nullptr;
     if (nco) {
