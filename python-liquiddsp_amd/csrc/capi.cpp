@@ -1720,27 +1720,32 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             q->hist_valid = 0;
             for (int i = 0; i < 3; i++) q->hist[i].ensure((size_t)hl * 8, q->device);
         }
-        const bool spec = !nospec && q->hist_valid >= hl;
         // chunk-parallel once it beats the one-lane loop: its latency is Wa approximate + W + 256
         // exact steps (~1.6 ms at bandwidth 0.01) against ~0.57 us per sample sequentially
         static const size_t parmin = (size_t)LDSP_KNOB("LDSP_AGC_PARMIN", 0L);
         const bool par = n >= (parmin ? parmin : (size_t)(0.7 * (0.16 * Wa + 0.43 * (W + 256)) / 0.57) + 256);
+        // below that, from ~300 samples: chunks approximating from the true state
+        // (latency 0.16 us per sample before the last chunk + 256 exact steps)
+        static const size_t tsamin = (size_t)LDSP_KNOB("LDSP_AGC_TSAMIN", 320L);
+        const bool tsa = !par && n >= tsamin;
+        const bool spec = !nospec && !tsa && q->hist_valid >= hl;
         k::SpecPlan p;
-        if (n > 0 && par) {
-            p.W = W;
+        if (n > 0 && (par || tsa)) {
+            p.W = tsa ? 0 : W;                 // tsa: every chunk from 1 on is checked against its predecessor
             p.Wa = Wa;
-            p.rounds = std::max(0, std::min(rounds, 6));
+            p.rounds = tsa ? 1 : std::max(0, std::min(rounds, 6));   // tsa: one run covers the rare deviation
             p.C = 256;
             p.nchunks = (long)((n + p.C - 1) / p.C);
             p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks), q->device);
             p.hist = q->hist[h3].p;
             p.H = spec ? (int)hl : 0;
+            p.tsa = tsa ? 1 : 0;
         }
         // the next call's history first: its front then waits for this copy only
         if (n > 0) k::delay_hist(dx, q->hist[h3].p, q->hist[(h3 + 1) % 3].p, n, (int)hl, e.stream);
         q->front.mark(e.stream);
         static const bool dbg = LDSP_KNOB("LDSP_DEBUG_AGC", 0) != 0;    // per-round re-run counters
-        if (n > 0 && par) {
+        if (n > 0 && (par || tsa)) {
             if (dbg) {
                 p.dbg = (unsigned*)p.scratch + (size_t)p.nchunks * 8;
                 LDSP_HIP(hipMemsetAsync(p.dbg, 0, 8 * sizeof(unsigned), e.stream));
@@ -1752,7 +1757,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         }
         q->ord.wait(e.stream);
         if (n > 0) {
-            if (par) {
+            if (par || tsa) {
                 if (spec) k::agc_spec_verify(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
                 else k::agc_spec_back(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
                 if (dbg) {

@@ -201,7 +201,7 @@ constexpr int kPow = kAgcPow;
 __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x, const float2* __restrict__ hist, long H,
                                                    long n, const AgcState* st, int C, int W, int Wa, long nch,
                                                    unsigned* __restrict__ sc, float2* __restrict__ y,
-                                                   uint8_t* __restrict__ status)
+                                                   uint8_t* __restrict__ status, int tsa)
 {
     LDSP_LATENCY_CRITICAL();
     const long chunk = (long)blockIdx.x * 64 + threadIdx.x;
@@ -212,7 +212,16 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
     const long s0 = chunk * C, s1 = min(n, s0 + C);
     long w0 = s0 - W;
     AgcReg r;
-    if (w0 <= lo) {
+    if (tsa) {
+        // small call (H = 0): the true state at x[0] is known, and the approximate
+        // loop started from it stays bit-identical to the exact one for thousands of
+        // samples in almost every case, so each chunk approximates from the call
+        // start to its own start (0.16 vs 0.43 us per step); a chunk whose start
+        // came out different is flagged against its predecessor and re-run.
+        r = AgcReg{p.g, p.y2p, p.mode, p.timer};
+        agc_run_approx(r, p, xe, 0, s0);
+        w0 = s0;
+    } else if (w0 <= lo) {
         w0 = lo;
         r = AgcReg{p.g, p.y2p, p.mode, p.timer};
     } else {
@@ -448,7 +457,7 @@ void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, vo
         LDSP_PROF(s, "k_agc_chunks");
         hipLaunchKernelGGL(k_agc_chunks, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, (const float2*)x,
                            (const float2*)p.hist, (long)p.H, (long)n, (const AgcState*)st, p.C, p.W, p.Wa, p.nchunks,
-                           (unsigned*)p.scratch, (float2*)y, status);
+                           (unsigned*)p.scratch, (float2*)y, status, p.tsa);
     }
     LDSP_HIP(hipGetLastError());
 }

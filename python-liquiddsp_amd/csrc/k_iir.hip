@@ -45,11 +45,17 @@ struct TfF {
     int nb, na, nv;
 };
 
+// Z: compile-time size class (sections / taps the loops are unrolled to; the
+// runtime counts still guard every term, so the operation sequence is the same
+// for any Z >= the filter's size).  Unrolled to the maximum, the guarded terms
+// of a first-order filter became a chain of ~50 selects per sample.
+template <int Z = kMaxTf>
 __device__ __forceinline__ float sos_step(const SosF& c, float (&v)[kMaxSos][3], float x)
 {
+    constexpr int KS = Z < kMaxSos ? Z : kMaxSos;
     float t = x;
 #pragma unroll
-    for (int s = 0; s < kMaxSos; s++) {
+    for (int s = 0; s < KS; s++) {
         if (s < c.nsos) {
             v[s][2] = v[s][1];
             v[s][1] = v[s][0];
@@ -61,21 +67,30 @@ __device__ __forceinline__ float sos_step(const SosF& c, float (&v)[kMaxSos][3],
 }
 
 // iirfilt_execute_norm: shift v; v0 = x - dot(a[1:], v[1:]); y = dot(b, v) (sequential dotprod)
+template <int Z = kMaxTf>
 __device__ __forceinline__ float tf_step(const TfF& c, float (&v)[kMaxTf], float x)
 {
+    constexpr int KT = Z < kMaxTf ? Z : kMaxTf;
 #pragma unroll
-    for (int i = kMaxTf - 1; i > 0; i--)
+    for (int i = KT - 1; i > 0; i--)
         if (i < c.nv) v[i] = v[i - 1];
     float r = 0.0f;
 #pragma unroll
-    for (int i = 1; i < kMaxTf; i++)
+    for (int i = 1; i < KT; i++)
         if (i < c.na) r = r + c.a[i] * v[i];
     v[0] = x - r;
     float y = 0.0f;
 #pragma unroll
-    for (int i = 0; i < kMaxTf; i++)
+    for (int i = 0; i < KT; i++)
         if (i < c.nb) y = y + c.b[i] * v[i];
     return y;
+}
+
+// size class of a filter for the templates above (host side)
+inline int iir_size_class(const IirDesc& d)
+{
+    const int m = d.sos ? d.nsos : d.nv;
+    return m <= 2 ? 2 : m <= 4 ? 4 : kMaxTf;
 }
 
 __device__ void load_sos(SosF& c, const IirDesc& d)
@@ -105,6 +120,7 @@ __device__ void load_tf(TfF& c, const IirDesc& d)
 __device__ __forceinline__ int fstate_size(const IirDesc& d) { return d.sos ? 3 * d.nsos : d.nv; }
 
 // --------------------------------------------------------------- sequential
+template <int Z>
 __global__ void k_iir_seq(IirDesc d, const float* __restrict__ x, long n, int ncomp, float* __restrict__ state,
                           float* __restrict__ y)
 {
@@ -120,7 +136,7 @@ __global__ void k_iir_seq(IirDesc d, const float* __restrict__ x, long n, int nc
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
             for (int k = 0; k < 3; k++) v[s][k] = s < d.nsos ? st[3 * s + k] : 0.0f;
-        for (long i = 0; i < n; i++) y[i * ncomp + c] = sos_step(cf, v, x[i * ncomp + c]);
+        for (long i = 0; i < n; i++) y[i * ncomp + c] = sos_step<Z>(cf, v, x[i * ncomp + c]);
 #pragma unroll
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
@@ -132,7 +148,7 @@ __global__ void k_iir_seq(IirDesc d, const float* __restrict__ x, long n, int nc
         float v[kMaxTf];
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++) v[i] = i < d.nv ? st[i] : 0.0f;
-        for (long i = 0; i < n; i++) y[i * ncomp + c] = tf_step(cf, v, x[i * ncomp + c]);
+        for (long i = 0; i < n; i++) y[i * ncomp + c] = tf_step<Z>(cf, v, x[i * ncomp + c]);
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++)
             if (i < d.nv) st[i] = v[i];
@@ -170,6 +186,7 @@ __device__ __forceinline__ void run_f32(StepF&& step, const float* __restrict__ 
 
 // --------------------------------------------------------------- speculative exact
 // scratch layout: [nchunks][2 (guess, end)][ncomp][fstate]  + flags
+template <int Z>
 __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* __restrict__ x, long n, int ncomp,
                                                         const float* __restrict__ state0, int C, int W, long nch,
                                                         float* __restrict__ sc, float* __restrict__ y)
@@ -195,13 +212,13 @@ __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* 
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
             for (int k = 0; k < 3; k++) v[s][k] = (from_true && s < d.nsos) ? state0[c * fs + 3 * s + k] : 0.0f;
-        run_f32<false>([&](float u) { return sos_step(cf, v, u); }, x, y, w0, s0, ncomp, c);
+        run_f32<false>([&](float u) { return sos_step<Z>(cf, v, u); }, x, y, w0, s0, ncomp, c);
 #pragma unroll
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
             for (int k = 0; k < 3; k++)
                 if (s < d.nsos) guess[3 * s + k] = v[s][k];
-        run_f32<true>([&](float u) { return sos_step(cf, v, u); }, x, y, s0, s1, ncomp, c);
+        run_f32<true>([&](float u) { return sos_step<Z>(cf, v, u); }, x, y, s0, s1, ncomp, c);
 #pragma unroll
         for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
@@ -213,11 +230,11 @@ __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* 
         float v[kMaxTf];
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++) v[i] = (from_true && i < d.nv) ? state0[c * fs + i] : 0.0f;
-        run_f32<false>([&](float u) { return tf_step(cf, v, u); }, x, y, w0, s0, ncomp, c);
+        run_f32<false>([&](float u) { return tf_step<Z>(cf, v, u); }, x, y, w0, s0, ncomp, c);
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++)
             if (i < d.nv) guess[i] = v[i];
-        run_f32<true>([&](float u) { return tf_step(cf, v, u); }, x, y, s0, s1, ncomp, c);
+        run_f32<true>([&](float u) { return tf_step<Z>(cf, v, u); }, x, y, s0, s1, ncomp, c);
 #pragma unroll
         for (int i = 0; i < kMaxTf; i++)
             if (i < d.nv) endst[i] = v[i];
@@ -249,6 +266,7 @@ __global__ void __launch_bounds__(64) k_iir_spec_flags(IirDesc d, int ncomp, int
 
 __device__ __forceinline__ uint32_t rl_u32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
 
+template <int Z>
 __global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* __restrict__ x, long n, int ncomp,
                                                         int C, int W, long nch, float* __restrict__ sc,
                                                         const unsigned long long* __restrict__ flags,
@@ -307,7 +325,7 @@ __global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* 
                 for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
                     for (int q = 0; q < 3; q++) v[s][q] = s < d.nsos ? ldnt(e + 3 * s + q) : 0.0f;
-                for (long i = s0; i < s1; i++) y[i * ncomp + c] = sos_step(cf, v, x[i * ncomp + c]);
+                for (long i = s0; i < s1; i++) y[i * ncomp + c] = sos_step<Z>(cf, v, x[i * ncomp + c]);
 #pragma unroll
                 for (int s = 0; s < kMaxSos; s++)
 #pragma unroll
@@ -319,7 +337,7 @@ __global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* 
                 float v[kMaxTf];
 #pragma unroll
                 for (int i = 0; i < kMaxTf; i++) v[i] = i < d.nv ? ldnt(e + i) : 0.0f;
-                for (long i = s0; i < s1; i++) y[i * ncomp + c] = tf_step(cf, v, x[i * ncomp + c]);
+                for (long i = s0; i < s1; i++) y[i * ncomp + c] = tf_step<Z>(cf, v, x[i * ncomp + c]);
 #pragma unroll
                 for (int i = 0; i < kMaxTf; i++)
                     if (i < d.nv) en[i] = v[i];
@@ -1138,8 +1156,13 @@ void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state,
     LDSP_REQUIRE(d.sos ? d.nsos <= kMaxSos : d.nv <= kMaxTf, "iir: filter order too high for the GPU kernels");
     {
         LDSP_PROF(s, "k_iir_seq");
-        hipLaunchKernelGGL(k_iir_seq, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, cplx ? 2 : 1, state,
-                           (float*)y);
+        const int z = iir_size_class(d);
+        auto launch = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, cplx ? 2 : 1, state, (float*)y);
+        };
+        if (z == 2) launch(k_iir_seq<2>);
+        else if (z == 4) launch(k_iir_seq<4>);
+        else launch(k_iir_seq<kMaxTf>);
     }
     LDSP_HIP(hipGetLastError());
 }
@@ -1160,10 +1183,16 @@ void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state
     if (n == 0) return;
     const int ncomp = cplx ? 2 : 1;
     const long work = p.nchunks * ncomp;
+    const int z = iir_size_class(d);
     {
         LDSP_PROF(s, "k_iir_spec_chunks");
-        hipLaunchKernelGGL(k_iir_spec_chunks, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, s, d, (const float*)x,
-                           (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks, (float*)p.scratch, (float*)y);
+        auto launch = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, s, d, (const float*)x, (long)n,
+                               ncomp, (const float*)state, p.C, p.W, p.nchunks, (float*)p.scratch, (float*)y);
+        };
+        if (z == 2) launch(k_iir_spec_chunks<2>);
+        else if (z == 4) launch(k_iir_spec_chunks<4>);
+        else launch(k_iir_spec_chunks<kMaxTf>);
     }
     LDSP_HIP(hipGetLastError());
     const int fs = d.sos ? 3 * d.nsos : d.nv;
@@ -1176,8 +1205,13 @@ void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state
     LDSP_HIP(hipGetLastError());
     {
         LDSP_PROF(s, "k_iir_spec_verify");
-        hipLaunchKernelGGL(k_iir_spec_verify, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, ncomp, p.C, p.W,
-                           p.nchunks, (float*)p.scratch, (const unsigned long long*)flags, state, (float*)y);
+        auto launch = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, ncomp, p.C, p.W, p.nchunks,
+                               (float*)p.scratch, (const unsigned long long*)flags, state, (float*)y);
+        };
+        if (z == 2) launch(k_iir_spec_verify<2>);
+        else if (z == 4) launch(k_iir_spec_verify<4>);
+        else launch(k_iir_spec_verify<kMaxTf>);
     }
     LDSP_HIP(hipGetLastError());
 }

@@ -1218,7 +1218,7 @@ void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m
 // Candidates + walk beat the one-lane loop (~0.57 us per sample) from about two
 // thousand samples: their latency is the warm-up plus one recorded chunk
 // (~0.94 ms), then the walk.
-static const size_t kParMin = (size_t)LDSP_KNOB("LDSP_PLL_PARMIN", 2048L);
+static const size_t kParMin = (size_t)LDSP_KNOB("LDSP_PLL_PARMIN", 1280L);
 bool pll_parallel(size_t n) { return n >= kParMin; }
 
 static PllIn pll_in(const PllCall& c)

@@ -141,6 +141,7 @@ struct SpecPlan {
     void* scratch;        // device scratch (states: start-guess and end per chunk)
     const void* hist = nullptr;   // AGC: the H input samples before x[0] (H > 0: every chunk speculative)
     int H = 0;
+    int tsa = 0;          // AGC small call: every chunk approximates from the true state up to its start
 };
 // scratch for iir_spec: chunk states + verifier flag words
 size_t spec_flags_offset(long nchunks, int ncomp, int fs);

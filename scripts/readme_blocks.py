@@ -15,17 +15,25 @@ import liquiddsp as L  # noqa: E402
 dev = torch.device("cuda", 0)
 blk, nblk = int(os.environ.get("BLK", "65536")), 64
 x = bench.synth_channel(blk * nblk, 0, dev)
-radio = bench.AMRadio(L)
-for i in range(4):
-    radio(x[i * blk:(i + 1) * blk])
-torch.cuda.synchronize()
-L._profile_reset()
-L._profile_enable(True)
-t0 = time.perf_counter()
-for i in range(nblk):
-    radio(x[i * blk:(i + 1) * blk])
-torch.cuda.synchronize()
-el = time.perf_counter() - t0
-L._profile_enable(False)
-kp = {k: round(v[1] / nblk * 1e3, 1) for k, v in L._profile_report().items()}
-print(json.dumps({"block": blk, "ms_per_block": round(el / nblk * 1e3, 3), "kernel_us_per_block": kp}))
+res = {"block": blk}
+for nst in (1, 2, 3, 4):
+    radio = bench.AMRadio(L)
+    strm = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+    for i in range(4):
+        with torch.cuda.stream(strm[i % nst]):
+            radio(x[i * blk:(i + 1) * blk])
+    torch.cuda.synchronize()
+    if nst == 1:
+        L._profile_reset()
+        L._profile_enable(True)
+    t0 = time.perf_counter()
+    for i in range(nblk):
+        with torch.cuda.stream(strm[i % nst]):
+            radio(x[i * blk:(i + 1) * blk])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if nst == 1:
+        L._profile_enable(False)
+        res["kernel_us_per_block"] = {k: round(v[1] / nblk * 1e3, 1) for k, v in L._profile_report().items()}
+    res[f"streams{nst}"] = {"ms_per_block": round(el / nblk * 1e3, 3), "Msamples_s": round(blk * nblk / el / 1e6, 1)}
+print(json.dumps(res))
