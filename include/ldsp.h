@@ -57,9 +57,18 @@ int ldsp_device_count(int *n);
 int ldsp_stream_synchronize(void *stream);
 
 /* Test hook: evaluate the loop transcendentals (ldsp_math.hpp) on the device.
- * fn: 0 exp, 1 log, 2 atan2(a, b), 3 tanh, 4 constrain (y as uint32 bits).
+ * fn: 0 exp, 1 log, 2 atan2(a, b), 3 tanh, 4 constrain (y as uint32 bits);
+ * 5 exp, 6 log through the loops' fast paths (lm_*_loop).
  * a, b, y are device pointers of n floats. */
 int ldsp_debug_math_eval(int fn, const float *a, const float *b, float *y, size_t n, void *stream);
+
+/* Test hook (host only, no device): check the loops' fast paths (ldsp_math.hpp
+ * lm_logf_fast, lm_expf_fast) against the general functions on every stride-th
+ * float bit pattern in [begin, end) that lies in the fast range (fn 0 log,
+ * 1 exp).  *checked: patterns in the fast range; *mismatches: how many differ in
+ * any bit. */
+int ldsp_debug_math_fastcheck(int fn, uint32_t begin, uint32_t end, uint32_t stride, uint64_t *checked,
+                              uint64_t *mismatches);
 
 /* Per-kernel device timing (no reference counterpart; measurement support for
  * bench.py).  While enabled every kernel launch is bracketed by a HIP event

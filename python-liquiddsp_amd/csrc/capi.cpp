@@ -17,6 +17,7 @@
 
 #include "design.hpp"
 #include "kernels.hpp"
+#include "ldsp_math.hpp"
 #include "ldsp_common.hpp"
 
 namespace ldsp {
@@ -942,9 +943,34 @@ int ldsp_stream_synchronize(void* stream)
 int ldsp_debug_math_eval(int fn, const float* a, const float* b, float* y, size_t n, void* stream)
 {
     return guard([&] {
-        LDSP_REQUIRE(fn >= 0 && fn <= 4, "math_eval: unknown function");
+        LDSP_REQUIRE(fn >= 0 && fn <= 6, "math_eval: unknown function");
         (void)current_device();
         k::math_eval(fn, a, b ? b : a, y, n, (hipStream_t)stream);
+    });
+}
+
+int ldsp_debug_math_fastcheck(int fn, uint32_t begin, uint32_t end, uint32_t stride, uint64_t* checked,
+                              uint64_t* mismatches)
+{
+    return guard([&] {
+        LDSP_REQUIRE(fn >= 0 && fn <= 1 && stride > 0 && checked && mismatches, "math_fastcheck: bad arguments");
+        uint64_t c = 0, bad = 0;
+        for (uint64_t u = begin; u < end; u += stride) {
+            const float a = bitsf((uint32_t)u);
+            if (fn == 0) {
+                if (lm_logf_fast_ok(a)) {
+                    c++;
+                    bad += fbits(lm_logf_fast(a)) != fbits(lm_logf(a));
+                }
+            } else if (fn == 1) {
+                if (lm_expf_fast_ok(a)) {
+                    c++;
+                    bad += fbits(lm_expf_fast(a)) != fbits(lm_expf(a));
+                }
+            }
+        }
+        *checked = c;
+        *mismatches = bad;
     });
 }
 
@@ -1720,12 +1746,15 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             q->hist_valid = 0;
             for (int i = 0; i < 3; i++) q->hist[i].ensure((size_t)hl * 8, q->device);
         }
-        // chunk-parallel once it beats the one-lane loop: its latency is Wa approximate + W + 256
-        // exact steps (~1.6 ms at bandwidth 0.01) against ~0.57 us per sample sequentially
+        // Latency per step on one lane (scripts/ubench/loop_lat.hip): approximate
+        // 0.06 us, exact 0.25 us.  Chunk-parallel from guesses (every chunk Wa
+        // approximate + W + 256 exact steps, ~0.8 us at bandwidth 0.01, overlapping
+        // the previous call) once a call is long enough that the true-start chunks
+        // below would take more than half of that.
         static const size_t parmin = (size_t)LDSP_KNOB("LDSP_AGC_PARMIN", 0L);
-        const bool par = n >= (parmin ? parmin : (size_t)(0.7 * (0.16 * Wa + 0.43 * (W + 256)) / 0.57) + 256);
+        const bool par = n >= (parmin ? parmin : std::max<size_t>(2048, (size_t)(0.5 * (0.06 * Wa + 0.25 * (W + 256)) / 0.06)));
         // below that, from ~300 samples: chunks approximating from the true state
-        // (latency 0.16 us per sample before the last chunk + 256 exact steps)
+        // (latency 0.06 us per sample before the last chunk + 256 exact steps)
         static const size_t tsamin = (size_t)LDSP_KNOB("LDSP_AGC_TSAMIN", 320L);
         const bool tsa = !par && n >= tsamin;
         const bool spec = !nospec && !tsa && q->hist_valid >= hl;

@@ -65,7 +65,12 @@ __device__ __forceinline__ void agc_squelch(AgcReg& r, const AgcState& p)
     }
 }
 
-// AGC(_execute) + the python-liquiddsp wrapper's zeroing (agc.hpp:114-126)
+// AGC(_execute) + the python-liquiddsp wrapper's zeroing (agc.hpp:114-126).
+// SQ = false: squelch disabled for the whole call (the state's mode is
+// SQ_DISABLED and stays so: no mode update, no zeroing), decided once per call
+// instead of per sample.  The gain update for y2p <= 1e-6 is a multiply by 1
+// (a select, not a branch around the transcendentals).
+template <bool SQ>
 __device__ __forceinline__ float2 agc_step(AgcReg& r, const AgcState& p, float2 x)
 {
     const float a = x.x * r.g, b = x.y * r.g;
@@ -75,12 +80,13 @@ __device__ __forceinline__ float2 agc_step(AgcReg& r, const AgcState& p, float2 
     if (p.locked) {
         y = make_float2(a, b);
     } else {
-        if (r.y2p > 1e-6f) r.g *= lm_expf(-0.5f * p.alpha * lm_logf(r.y2p));
+        const float f = lm_expf_loop(-0.5f * p.alpha * lm_logf_loop(r.y2p));
+        r.g *= (r.y2p > 1e-6f) ? f : 1.0f;
         r.g = (r.g > 1e6f) ? 1e6f : r.g;
-        agc_squelch(r, p);
+        if (SQ) agc_squelch(r, p);
         y = make_float2(a * p.scale, b * p.scale);
     }
-    if (r.mode == SQ_SIGNALLO || r.mode == SQ_ENABLED) {
+    if (SQ && (r.mode == SQ_SIGNALLO || r.mode == SQ_ENABLED)) {
         y.x *= 0.0f;
         y.y *= 0.0f;
     }
@@ -90,6 +96,7 @@ __device__ __forceinline__ float2 agc_step(AgcReg& r, const AgcState& p, float2 
 // Approximate step (hardware v_log_f32 / v_exp_f32, float32 smoothing): used
 // only to bring a chunk's guessed state within a few ulps of the true
 // trajectory before the exact warm-up (never for outputs).
+template <bool SQ>
 __device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, float2 x)
 {
     const float a = x.x * r.g, b = x.y * r.g;
@@ -102,62 +109,89 @@ __device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, fl
         // scaled by alpha/2, far below an ulp of the factor), exp by a short series.  The
         // factor then rounds like lm_expf's almost always, so this trajectory tracks the
         // exact one within a few ulps instead of drifting by its own rounding noise.
-        if (r.y2p > 1e-6f) {
-            const float t = -0.5f * p.alpha * (__builtin_amdgcn_logf(r.y2p) * 0.69314718056f);
-            const float u = t * (1.0f + t * (0.5f + t * (0.16666667f + t * 0.041666668f)));
-            r.g *= 1.0f + u;
-        }
+        const float t = -0.5f * p.alpha * (__builtin_amdgcn_logf(r.y2p) * 0.69314718056f);
+        const float u = t * (1.0f + t * (0.5f + t * (0.16666667f + t * 0.041666668f)));
+        r.g *= (r.y2p > 1e-6f) ? 1.0f + u : 1.0f;
         r.g = (r.g > 1e6f) ? 1e6f : r.g;
-        agc_squelch(r, p);
+        if (SQ) agc_squelch(r, p);
     }
 }
 
+// Both loops run whole batches of kA / kB samples without a per-sample bound
+// check (the lanes of a chunk kernel all run the same length, but the compiler
+// cannot know that: a per-sample check became an exec-mask branch around every
+// step), loads software-pipelined one batch ahead (addresses clamped, so the
+// prefetch needs no check either), then the tail sample by sample.  In a
+// one-wave dependent chain every instruction costs ~4 cycles of issue.
+template <bool SQ, class X>
+__device__ __forceinline__ void agc_run_approx_t(AgcReg& r, const AgcState& p, const X& x, long a, long b)
+{
+    constexpr int kA = 16;
+    if (a >= b) return;
+    const long full = a + (b - a) / kA * kA;
+    float2 nx[kA];
+#pragma unroll
+    for (int j = 0; j < kA; j++) nx[j] = x[min(a + j, b - 1)];
+    long i = a;
+    for (; i < full; i += kA) {
+        float2 cx[kA];
+#pragma unroll
+        for (int j = 0; j < kA; j++) cx[j] = nx[j];
+#pragma unroll
+        for (int j = 0; j < kA; j++) nx[j] = x[min(i + kA + j, b - 1)];
+#pragma unroll
+        for (int j = 0; j < kA; j++) agc_step_approx<SQ>(r, p, cx[j]);
+    }
+    for (; i < b; i++) agc_step_approx<SQ>(r, p, x[i]);
+}
 template <class X>
 __device__ __forceinline__ void agc_run_approx(AgcReg& r, const AgcState& p, const X& x, long a, long b)
 {
-    constexpr int kA = 8;
-    for (long i = a; i < b; i += kA) {
-        float2 cx[kA];
-#pragma unroll
-        for (int j = 0; j < kA; j++) cx[j] = x[min(i + j, b - 1)];
-#pragma unroll
-        for (int j = 0; j < kA; j++)
-            if (i + j < b) agc_step_approx(r, p, cx[j]);
-    }
+    if (p.mode == SQ_DISABLED) agc_run_approx_t<false>(r, p, x, a, b);
+    else agc_run_approx_t<true>(r, p, x, a, b);
 }
 
-// Run the AGC over x[a, b) with the loads software-pipelined kB samples ahead
-// (they are off the gain recurrence's dependence chain).  OUT: write y/status.
+// Run the AGC over x[a, b) (exact).  OUT: write y/status.
 constexpr int kB = 8;
+template <bool OUT, bool SQ, class X>
+__device__ __forceinline__ void agc_run_t(AgcReg& r, const AgcState& p, const X& x, long a, long b,
+                                          float2* __restrict__ y, uint8_t* __restrict__ status)
+{
+    if (a >= b) return;
+    const long full = a + (b - a) / kB * kB;
+    float2 nx[kB];
+#pragma unroll
+    for (int j = 0; j < kB; j++) nx[j] = x[min(a + j, b - 1)];
+    long i = a;
+    for (; i < full; i += kB) {
+        float2 cx[kB];
+#pragma unroll
+        for (int j = 0; j < kB; j++) cx[j] = nx[j];
+#pragma unroll
+        for (int j = 0; j < kB; j++) nx[j] = x[min(i + kB + j, b - 1)];
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            const float2 v = agc_step<SQ>(r, p, cx[j]);
+            if (OUT) {
+                y[i + j] = v;
+                if (status) status[i + j] = (uint8_t)r.mode;
+            }
+        }
+    }
+    for (; i < b; i++) {
+        const float2 v = agc_step<SQ>(r, p, x[i]);
+        if (OUT) {
+            y[i] = v;
+            if (status) status[i] = (uint8_t)r.mode;
+        }
+    }
+}
 template <bool OUT, class X>
 __device__ __forceinline__ void agc_run(AgcReg& r, const AgcState& p, const X& x, long a, long b,
                                         float2* __restrict__ y, uint8_t* __restrict__ status)
 {
-    if (a >= b) return;
-    float2 nx[kB];
-#pragma unroll
-    for (int j = 0; j < kB; j++) nx[j] = x[min(a + j, b - 1)];
-    for (long i = a; i < b; i += kB) {
-        float2 cx[kB];
-#pragma unroll
-        for (int j = 0; j < kB; j++) cx[j] = nx[j];
-        if (i + kB < b) {
-#pragma unroll
-            for (int j = 0; j < kB; j++) nx[j] = x[min(i + kB + j, b - 1)];
-        }
-#pragma unroll
-        for (int j = 0; j < kB; j++) {
-            if (i + j < b) {
-                const float2 v = agc_step(r, p, cx[j]);
-                if (OUT) {
-                    y[i + j] = v;
-                    if (status) status[i + j] = (uint8_t)r.mode;
-                } else {
-                    (void)v;
-                }
-            }
-        }
-    }
+    if (p.mode == SQ_DISABLED) agc_run_t<OUT, false>(r, p, x, a, b, y, status);
+    else agc_run_t<OUT, true>(r, p, x, a, b, y, status);
 }
 
 // One lane runs the loop; the wave stages the input through LDS 2048 samples
@@ -430,6 +464,8 @@ __global__ void k_math_eval(int fn, const float* __restrict__ a, const float* __
     case 2: r = lm_atan2f(a[i], b[i]); break;
     case 3: r = lm_tanhf(a[i]); break;
     case 4: r = __uint_as_float(lm_constrain(a[i])); break;
+    case 5: r = lm_expf_loop(a[i]); break;
+    case 6: r = lm_logf_loop(a[i]); break;
     default: break;
     }
     y[i] = r;

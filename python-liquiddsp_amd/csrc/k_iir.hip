@@ -156,31 +156,34 @@ __global__ void k_iir_seq(IirDesc d, const float* __restrict__ x, long n, int nc
 }
 
 // x[a, b) of component c through a float32 step, loads batched 8 ahead (off the
-// recurrence's dependence chain); WRITE stores the outputs.
+// recurrence's dependence chain); whole batches without a per-sample bound check,
+// then the tail.  WRITE stores the outputs.
 template <bool WRITE, class StepF>
 __device__ __forceinline__ void run_f32(StepF&& step, const float* __restrict__ x, float* __restrict__ y, long a,
                                         long b, int ncomp, int c)
 {
     constexpr int kQ = 8;
     if (a >= b) return;
+    const long full = a + (b - a) / kQ * kQ;
     float nx[kQ];
 #pragma unroll
     for (int j = 0; j < kQ; j++) nx[j] = x[min(a + j, b - 1) * ncomp + c];
-    for (long i = a; i < b; i += kQ) {
+    long i = a;
+    for (; i < full; i += kQ) {
         float cx[kQ];
 #pragma unroll
         for (int j = 0; j < kQ; j++) cx[j] = nx[j];
-        if (i + kQ < b) {
 #pragma unroll
-            for (int j = 0; j < kQ; j++) nx[j] = x[min(i + kQ + j, b - 1) * ncomp + c];
-        }
+        for (int j = 0; j < kQ; j++) nx[j] = x[min(i + kQ + j, b - 1) * ncomp + c];
 #pragma unroll
         for (int j = 0; j < kQ; j++) {
-            if (i + j < b) {
-                const float o = step(cx[j]);
-                if (WRITE) y[(i + j) * ncomp + c] = o;
-            }
+            const float o = step(cx[j]);
+            if (WRITE) y[(i + j) * ncomp + c] = o;
         }
+    }
+    for (; i < b; i++) {
+        const float o = step(x[i * ncomp + c]);
+        if (WRITE) y[i * ncomp + c] = o;
     }
 }
 

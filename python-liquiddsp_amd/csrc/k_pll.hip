@@ -157,15 +157,35 @@ __device__ __forceinline__ const float2* x1_ptr(const PllIn& in, long i)
 }
 
 // Run the loop over [a, b) with the inputs software-pipelined kB samples ahead
-// (the loads are off the theta dependence chain).  REC: record the candidate,
+// (the loads are off the theta dependence chain), whole batches without a
+// per-sample bound check (in a one-wave chain each exec-mask branch costs
+// several issue slots per sample), then the tail.  REC: record the candidate,
 // write its output, count the chunk's entries.
 constexpr int kB = 8;
+template <bool REC>
+__device__ __forceinline__ void cand_step(const PllIn& in, const float* tab, long s, long a, long b, float2 c0,
+                                          float2 c1, float alpha, float beta, uint32_t& theta, uint32_t& d,
+                                          const CandBuf& cb, uint4& rec, float& yo, uint32_t& nent)
+{
+    const uint32_t ic = tidx(theta);
+    const Kick kc = pll_eval(tab, ic, c0, c1, alpha, beta, in.mod_index, in.costas);
+    if (REC) {
+        const uint32_t w = theta + (1u << 21);
+        rec = make_uint4(w, kc.k1, kc.k2, __float_as_uint(kc.out));
+        yo = kc.out;
+        nent += (risky(w, cb.B) || s == a || s == b - 1) ? 1u : 0u;
+    }
+    d += kc.k1;
+    theta += kc.k2 + d;
+}
+
 template <bool REC>
 __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long a, long b, float alpha, float beta,
                                          uint32_t& theta, uint32_t& d, const CandBuf& cb, float* __restrict__ y,
                                          uint32_t& nent)
 {
     if (a >= b) return;
+    const long full = a + (b - a) / kB * kB;
     float2 n0[kB], n1[kB];
 #pragma unroll
     for (int j = 0; j < kB; j++) {
@@ -173,20 +193,19 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
         n0[j] = in.x0[i];
         n1[j] = *x1_ptr(in, i);
     }
-    for (long i = a; i < b; i += kB) {
+    long i = a;
+    for (; i < full; i += kB) {
         float2 c0[kB], c1[kB];
 #pragma unroll
         for (int j = 0; j < kB; j++) {
             c0[j] = n0[j];
             c1[j] = n1[j];
         }
-        if (i + kB < b) {
 #pragma unroll
-            for (int j = 0; j < kB; j++) {
-                const long ii = min(i + kB + j, b - 1);
-                n0[j] = in.x0[ii];
-                n1[j] = *x1_ptr(in, ii);
-            }
+        for (int j = 0; j < kB; j++) {
+            const long ii = min(i + kB + j, b - 1);
+            n0[j] = in.x0[ii];
+            n1[j] = *x1_ptr(in, ii);
         }
         // REC: the group's records and outputs are kept in registers and stored
         // back to back after it, so each lane's 128 B of records and 32 B of
@@ -196,35 +215,22 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
         uint4 r0[kB];
         float yo[kB];
 #pragma unroll
-        for (int j = 0; j < kB; j++) {
-            if (i + j < b) {
-                const uint32_t ic = tidx(theta);
-                const Kick kc = pll_eval(tab, ic, c0[j], c1[j], alpha, beta, in.mod_index, in.costas);
-                if (REC) {
-                    const long s = i + j;
-                    const uint32_t w = theta + (1u << 21);
-                    r0[j] = make_uint4(w, kc.k1, kc.k2, __float_as_uint(kc.out));
-                    yo[j] = kc.out;
-                    nent += (risky(w, cb.B) || s == a || s == b - 1) ? 1u : 0u;
-                }
-                d += kc.k1;
-                theta += kc.k2 + d;
-            }
-        }
+        for (int j = 0; j < kB; j++)
+            cand_step<REC>(in, tab, i + j, a, b, c0[j], c1[j], alpha, beta, theta, d, cb, r0[j], yo[j], nent);
         if (REC) {
-            if (i + kB <= b) {
 #pragma unroll
-                for (int j = 0; j < kB; j++) cb.rec[i + j] = r0[j];
+            for (int j = 0; j < kB; j++) cb.rec[i + j] = r0[j];
 #pragma unroll
-                for (int j = 0; j < kB; j++) y[i + j] = yo[j];
-            } else {
-#pragma unroll
-                for (int j = 0; j < kB; j++)
-                    if (i + j < b) {
-                        cb.rec[i + j] = r0[j];
-                        y[i + j] = yo[j];
-                    }
-            }
+            for (int j = 0; j < kB; j++) y[i + j] = yo[j];
+        }
+    }
+    for (; i < b; i++) {
+        uint4 r0;
+        float yo;
+        cand_step<REC>(in, tab, i, a, b, in.x0[i], *x1_ptr(in, i), alpha, beta, theta, d, cb, r0, yo, nent);
+        if (REC) {
+            cb.rec[i] = r0;
+            y[i] = yo;
         }
     }
 }

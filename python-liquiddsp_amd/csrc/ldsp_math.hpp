@@ -199,6 +199,100 @@ __host__ __device__ inline float lm_tanhf(float x)
     return r;
 }
 
+// ---- Fast paths for the serial loops.  A wave running one dependent chain
+// issues one wave64 instruction per ~4 cycles, so a loop step costs about its
+// instruction count (scripts/ubench/loop_lat.hip: lm_logf 184 ns, lm_expf 144,
+// lm_atan2f 299 against 7 ns for a dependent mul + add).  The functions below
+// are the same operation sequences as lm_logf / lm_expf restricted to the
+// common argument range, where most of fdlibm's cases (zero, subnormal,
+// infinite, NaN, |f| < 2^-20, reduced exponent) cannot occur; callers test
+// *_fast_ok and take the general function otherwise.  (The same treatment of
+// lm_atan2f measured slower: its cases are already selects, and a range test
+// plus a branch to the general code cost more than the few selects saved.)  Equality with the general
+// functions over the whole fast range: ldsp_debug_math_fastcheck
+// (tests/test_capi_host.py samples it; scripts/analysis/check_fast_math.py runs
+// every float).
+
+// n / d correctly rounded, for operands that need no range scaling (|d| in
+// [1, 4), n zero or |n| in [2^-64, 4)): on the device the compiler's own IEEE
+// sequence (reciprocal, one Newton step, two residual corrections) without its
+// v_div_scale / v_div_fmas scaling and v_div_fixup special cases, which such
+// operands never trigger -- the same bits in 8 instructions instead of 11.
+__host__ __device__ inline float div_noscale(float n, float d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r = __builtin_amdgcn_rcpf(d);
+    float e = fmaf(-d, r, 1.0f);
+    r = fmaf(e, r, r);
+    float q = n * r;
+    e = fmaf(-d, q, n);
+    q = fmaf(e, r, q);
+    e = fmaf(-d, q, n);
+    return fmaf(e, r, q);
+#else
+    return n / d;
+#endif
+}
+
+// lm_logf for normal, positive, finite x with |f| >= 2^-20
+__host__ __device__ inline bool lm_logf_fast_ok(float x)
+{
+    const int32_t ix = (int32_t)fbits(x);
+    return ix >= 0x00800000 && ix < 0x7f800000 && (0x007fffff & (15 + (ix & 0x007fffff))) >= 16;
+}
+__host__ __device__ inline float lm_logf_fast(float x)
+{
+    constexpr float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f;
+    constexpr float Lg1 = 6.6666668653e-01f, Lg2 = 4.0000000596e-01f, Lg3 = 2.8571429849e-01f,
+                    Lg4 = 2.2222198546e-01f, Lg5 = 1.8183572590e-01f, Lg6 = 1.5313838422e-01f,
+                    Lg7 = 1.4798198640e-01f;
+    const int32_t ix = (int32_t)fbits(x);
+    const int32_t m = ix & 0x007fffff;
+    const int32_t i = (m + (0x95f64 << 3)) & 0x800000;
+    const int32_t k = (ix >> 23) - 127 + (i >> 23);
+    const float f = bitsf((uint32_t)(m | (i ^ 0x3f800000))) - 1.0f;
+    const float s = div_noscale(f, 2.0f + f);            // f in (-0.293, 0.415], f == 0 or |f| >= 2^-23
+    const float dk = (float)k;
+    const float z = s * s;
+    const float w = z * z;
+    const float t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const float t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const float R = t2 + t1;
+    const bool ii = ((m - (0x6147a << 3)) | ((0x6b851 << 3) - m)) > 0;
+    const float hfsq = 0.5f * f * f;
+    if (k == 0) return ii ? f - (hfsq - s * (hfsq + R)) : f - s * (f - R);
+    return ii ? dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f)
+              : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// lm_expf for 2^-28 <= |x| <= 0.5 ln2 (no argument reduction: k = 0)
+__host__ __device__ inline bool lm_expf_fast_ok(float x)
+{
+    const uint32_t ix = fbits(x) & 0x7fffffffu;
+    return ix >= 0x31800000u && ix <= 0x3eb17218u;
+}
+__host__ __device__ inline float lm_expf_fast(float x)
+{
+    constexpr float P1 = 1.6666667163e-01f, P2 = -2.7777778450e-03f, P3 = 6.6137559770e-05f,
+                    P4 = -1.6533901999e-06f, P5 = 4.1381369442e-08f;
+    const float t = x * x;
+    const float c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    return 1.0f - (div_noscale(x * c, c - 2.0f) - x);    // c - 2 ~ -2, |x c| in [2^-57, 0.25]
+}
+
+// The general function, through the fast path when x is in its range (a
+// branch, not a select: a wave whose lanes are all in range skips the general
+// code).
+__host__ __device__ inline float lm_logf_loop(float x)
+{
+    if (__builtin_expect(lm_logf_fast_ok(x), 1)) return lm_logf_fast(x);
+    return lm_logf(x);
+}
+__host__ __device__ inline float lm_expf_loop(float x)
+{
+    if (__builtin_expect(lm_expf_fast_ok(x), 1)) return lm_expf_fast(x);
+    return lm_expf(x);
+}
 // NCO(_constrain) (liquid nco.proto.c): radians -> 32-bit fixed-point phase.
 // p is formed in double (1/2pi literal is double), the fraction in float
 // ((float)(long)p == truncf(p)), the negative wrap in double, and the

@@ -274,3 +274,13 @@ def test_iir_freqresponse_all_types(lib, ft, bt):
         got.append(complex(re_.value, im_.value))
     assert np.max(np.abs(np.abs(got) - np.abs(hr))) < 1e-4
     lib.ldsp_iirfilt_destroy(q)
+
+
+@pytest.mark.parametrize("fn", [0, 1])
+def test_loop_fast_math_equals_general(lib, fn):
+    """lm_logf_fast / lm_expf_fast (the AGC loop's fast paths) give the general
+    functions' bits on a sample of every float in their ranges (host build of
+    ldsp_math.hpp; scripts/analysis/check_fast_math.py runs every float)."""
+    checked, bad = C.c_uint64(), C.c_uint64()
+    assert lib.ldsp_debug_math_fastcheck(fn, 0, 0xFFFFFFFF, 4099, C.byref(checked), C.byref(bad)) == 0
+    assert checked.value > 100_000 and bad.value == 0, (checked.value, bad.value)

@@ -67,6 +67,19 @@ def test_device_math_bitwise(ld, ora, rng):
             assert np.array_equal(np.isnan(got), np.isnan(ref))
             got, ref = got[~np.isnan(ref)], ref[~np.isnan(ref)]
         assert_bitwise(got, ref)
+    # the AGC loop's fast paths (fn 5 exp, 6 log: lm_*_loop, scaling-free division
+    # on the device) must give the general functions' bits everywhere, in and out
+    # of their fast ranges
+    loop_cases = {5: np.float32(np.concatenate([rng.uniform(-0.35, 0.35, n // 2), rng.uniform(-30, 30, n // 4),
+                                                np.ldexp(rng.uniform(-1, 1, n // 4), rng.integers(-40, -20, n // 4))])),
+                  6: np.float32(np.concatenate([rng.uniform(0.5, 2.0, n // 2), np.exp(rng.uniform(-80, 80, n // 4)),
+                                                1.0 + np.ldexp(rng.uniform(-1, 1, n // 4), -21)]))}
+    for fn, a in loop_cases.items():
+        ta = torch.from_numpy(a).cuda()
+        ty = torch.empty_like(ta)
+        ld._math_eval(fn, ta.data_ptr(), ta.data_ptr(), ty.data_ptr(), a.size, 0)
+        torch.cuda.synchronize()
+        assert_bitwise(ty.cpu().numpy(), ora.math_eval("exp" if fn == 5 else "log", a, None))
     th = np.float32(rng.uniform(-20, 20, 4096))
     ta = torch.from_numpy(th).cuda()
     ty = torch.empty_like(ta)
