@@ -208,7 +208,10 @@ __host__ __device__ inline float lm_tanhf(float x)
 // infinite, NaN, |f| < 2^-20, reduced exponent) cannot occur; callers test
 // *_fast_ok and take the general function otherwise.  (The same treatment of
 // lm_atan2f measured slower: its cases are already selects, and a range test
-// plus a branch to the general code cost more than the few selects saved.)  Equality with the general
+// plus a branch to the general code cost more than the few selects saved; a
+// near-lock atan2 (|y / x| < 0.4375: no reduction, no second division) behind a
+// wave-uniform test slowed the PLL candidates by 20 %: their 64 lanes run 64
+// chunks, and one lane out of range sends the wave through both paths.)  Equality with the general
 // functions over the whole fast range: ldsp_debug_math_fastcheck
 // (tests/test_capi_host.py samples it; scripts/analysis/check_fast_math.py runs
 // every float).
