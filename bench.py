@@ -480,6 +480,19 @@ def components(L, device, reps=5):
                              "blocks_65536_Msamples_s": round(len(blocks) * 65536 / el / 1e6, 1),
                              "outputs_per_65536": nout}
     del xs, blocks
+    # the chain's first filter fed the SDR wire format.  Two
+    # calls (bytes_to_iq, then the cheby2 IIR) against ComplexIIRFilter.from_bytes,
+    # which converts int16 IQ in the blocked scan's loads (4 B / sample per pass).
+    raw = torch.randint(-32768, 32768, (2 * n,), generator=g, device=device, dtype=torch.int32).to(torch.int16)
+    iir = dict(filter_type="cheby2", order=8, Fc=15000 / 2000000)
+    fa, fb = L.ComplexIIRFilter(**iir), L.ComplexIIRFilter(**iir)
+    ta = timed(lambda: fa(L.bytes_to_iq(raw)))
+    tb = timed(lambda: fb.from_bytes(raw))
+    out["iq16_iir_64Mi"] = {"two_calls_ms": round(sum(ta.values()), 4), "fused_ms": round(sum(tb.values()), 4),
+                            "two_calls_kernels": {k: round(v, 4) for k, v in ta.items()},
+                            "fused_kernels": {k: round(v, 4) for k, v in tb.items()},
+                            "alg_bytes_fused": 12 * n, "alg_bytes_two_calls": 24 * n}
+    del raw
     n = 256 << 20
     xs = torch.complex(torch.randn(n, generator=g, device=device), torch.randn(n, generator=g, device=device))
     nco = L.NCO("nco")

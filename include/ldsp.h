@@ -192,6 +192,15 @@ int ldsp_iirfilt_get_nsos(ldsp_iirfilt_t q, unsigned int *nsos);
 int ldsp_iirfilt_get_sos(ldsp_iirfilt_t q, float *B, float *A);
 int ldsp_iirfilt_freqresponse(ldsp_iirfilt_t q, float f, float *re, float *im);
 int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void *x, size_t n, void *y, int mem, void *stream);
+/* bytes_to_iq fused into the filter (replaces the pair
+ * `filter(bytes_to_iq(raw))`, src/utility.hpp:61-69 + iirfilter.hpp:292-298):
+ * x holds n native int16 (I, Q) pairs (4 n bytes), each converted to
+ * (float)v / 32767.0f exactly as bytes_to_iq does; y receives n complex64
+ * outputs, the same bits as ldsp_bytes_to_iq followed by ldsp_iirfilt_execute.
+ * Complex filters only (LDSP_EINVAL otherwise).  The blocked float64 scan (the
+ * default fast mode) converts on load, so the input is read at 4 B per sample;
+ * the exact and speculative paths convert with one extra pass first. */
+int ldsp_iirfilt_execute_iq16(ldsp_iirfilt_t q, const void *x, size_t n, void *y, int mem, void *stream);
 
 /* ------------------------------------------------------------------------
  * AGC: agc_crcf.  Replaces AGC (src/agc.hpp:4-149).  execute implements

@@ -327,6 +327,7 @@ struct IirObj {
     // into st64b; the two are swapped after the call)
     int J1p = 0;
     DevBuf p1mats, p1agg, p1flags, p1ticket, st64b;
+    DevBuf iq;                        // int16 IQ converted for the paths that do not read it themselves
     long p1_nblk_cap = 0;
     unsigned p1_epoch = 0;
     bool state_in64 = false;          // where the authoritative state lives
@@ -1524,21 +1525,33 @@ int ldsp_iirfilt_freqresponse(ldsp_iirfilt_t q, float f, float* re, float* im)
     });
 }
 
-int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
+// iq16: x is n int16 (I, Q) pairs (bytes_to_iq's input); the blocked float64
+// scan converts them on load, the other paths after a k_bytes_to_iq pass.
+static int iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int mem, void* stream, bool iq16)
 {
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "iirfilt_execute: NULL buffer");
+        LDSP_REQUIRE(!iq16 || q->cplx, "iirfilt_execute_iq16: the filter is real; int16 IQ input needs a complex one");
         const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
         const Exec e = make_exec(q->device, mem, stream, bd);
         q->ord.wait(e.stream);
         const size_t bytes = n * (q->cplx ? 8 : 4);
-        const void* dx = q->stg.dev_in(e, x, bytes);
+        const void* dx = q->stg.dev_in(e, x, iq16 ? n * 4 : bytes);
         void* dy = q->stg.dev_out(e, y, bytes);
         if (n > 0) {
             const k::IirDesc d = q->desc();
+            const bool blk = !(q->spec_W > 0 && q->spec_W <= 16384) && q->mode != LDSP_MODE_EXACT &&
+                             !(q->J1p > 0 && LDSP_KNOB("LDSP_IIR_1P", 0)) && q->D <= k::kIirBlkMaxD &&
+                             !LDSP_KNOB("LDSP_IIR_OLDSCAN", 0);
+            if (iq16 && !blk) {                    // not fused: convert first
+                void* cx = q->iq.ensure(n * 8, q->device);
+                k::bytes_to_iq(dx, cx, n, e.stream);
+                dx = cx;
+                iq16 = false;
+            }
             if (q->spec_W > 0 && q->spec_W <= 16384) {
                 // fast-decaying filter: speculative exact chunks (same bits as sequential)
                 q->state_to(false, e.stream);
@@ -1565,7 +1578,7 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
             } else if (q->D <= k::kIirBlkMaxD && !LDSP_KNOB("LDSP_IIR_OLDSCAN", 0)) {
                 q->state_to(true, e.stream);
                 const k::IirBlkPlan p = q->blk_plan(n);
-                k::iir_blk(q->cplx, d, q->b.data(), q->a.data(), dx, n, q->st64.as<double>(), p, dy, e.stream);
+                k::iir_blk(q->cplx, d, q->b.data(), q->a.data(), dx, n, q->st64.as<double>(), p, dy, e.stream, iq16);
             } else {
                 q->state_to(true, e.stream);
                 const k::IirScanPlan p = q->scan_plan(n);
@@ -1576,6 +1589,14 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int
         q->last = e.stream;
         q->stg.finish(e, y, bytes);
     });
+}
+int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
+{
+    return iirfilt_execute(q, x, n, y, mem, stream, false);
+}
+int ldsp_iirfilt_execute_iq16(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
+{
+    return iirfilt_execute(q, x, n, y, mem, stream, true);
 }
 
 // ---------------------------------------------------------------- AGC
@@ -1940,6 +1961,9 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     k::pll_front(c, e.stream);
     const bool par = k::pll_parallel(n);
     if (par) q->front.mark(e.stream);     // the sequential loop writes the guess itself: mark after it
+    // (A dedicated high-priority walker queue was measured: the ~25 us between
+    // walks stayed -- it is the dispatcher waiting for a whole CU to drain for the
+    // walker's 135 KiB of LDS, not the cross-queue event -- and the chain slowed.)
     q->ord.wait(e.stream);
     k::pll_back(c, e.stream);
     q->ord.mark(e.stream);                // the true PLL state: the next call's walk may start

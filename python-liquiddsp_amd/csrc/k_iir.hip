@@ -670,9 +670,24 @@ __device__ __forceinline__ void mv_acc(const double* __restrict__ M, const doubl
 // The staging tiles and the scan buffer share LDS (they are used in separate
 // phases, fenced by __syncthreads): 35 KB per block, and at most 168 VGPRs, so
 // three blocks (12 waves) fit a CU to hide the HBM latency of the tile stream.
-template <int NC, int D, bool FINAL, class Step>
+// (float)v / 32767.0f for int16 v without the IEEE division sequence: the
+// product with fl(1/32767) corrected by one fma residual step.  Equal to the
+// correctly rounded quotient for all 65 536 inputs
+// (scripts/analysis/check_iq16_div.py, tests/test_oracle_math.py).
+__device__ __forceinline__ float iq16_to_f(short v)
+{
+    constexpr float d = 32767.0f, r = 1.0f / 32767.0f;
+    const float f = (float)v;
+    const float q0 = f * r;
+    return fmaf(fmaf(-q0, d, f), r, q0);
+}
+
+// IQ16: the input is the SDR wire format (int16 I, Q pairs) converted on load
+// exactly as bytes_to_iq (utility.hpp:61-69: (float)v / 32767.0f), so a chain
+// fed raw IQ reads 4 B per sample in both passes instead of 8.
+template <int NC, int D, bool FINAL, class Step, bool IQ16 = false>
 __global__ void __launch_bounds__(kBN) __attribute__((amdgpu_waves_per_eu(3)))
-k_iir_blk(Step step, const float* __restrict__ xf, long n, long nch, const double* __restrict__ AL,
+k_iir_blk(Step step, const void* __restrict__ xf, long n, long nch, const double* __restrict__ AL,
           double* __restrict__ Lloc, const double* __restrict__ BS, double* __restrict__ BL,
           double* __restrict__ state64, float* __restrict__ yf)
 {
@@ -683,7 +698,9 @@ k_iir_blk(Step step, const float* __restrict__ xf, long n, long nch, const doubl
     __shared__ __attribute__((aligned(16))) char lds[kStage > kScn ? kStage : kScn];
     T (*stage)[64 * kRow] = reinterpret_cast<T (*)[64 * kRow]>(lds);
     double (*scn)[NC][D] = reinterpret_cast<double (*)[NC][D]>(lds);
+    static_assert(!IQ16 || NC == 2, "int16 IQ input is complex");
     const T* __restrict__ x = (const T*)xf;
+    const short2* __restrict__ x16 = (const short2*)xf;
     T* __restrict__ y = (T*)yf;
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -699,14 +716,18 @@ k_iir_blk(Step step, const float* __restrict__ xf, long n, long nch, const doubl
     // Runs this lane's chunk over the staged tiles from state v.
     auto run = [&](auto write_tag) {
         constexpr bool WRITE = decltype(write_tag)::value;
-        T nxt[kBT];
+        // raw loads stay in flight across the tile; int16 pairs are converted
+        // only when staged (a conversion next to its load would wait for it)
+        using Raw = std::conditional_t<IQ16, int, T>;
+        Raw nxt[kBT];
         auto fetch = [&](int k) {
 #pragma unroll
             for (int q = 0; q < kBT; q++) {
                 const int e = lane + 64 * q;
                 const long gi = wbase + (long)(e >> 4) * kBC + k * kBT + (e & 15);
-                T z{};
-                nxt[q] = gi < n ? x[gi] : z;
+                Raw z{};
+                if constexpr (IQ16) nxt[q] = gi < n ? ((const int*)x16)[gi] : z;
+                else nxt[q] = gi < n ? x[gi] : z;
             }
         };
         fetch(0);
@@ -714,7 +735,11 @@ k_iir_blk(Step step, const float* __restrict__ xf, long n, long nch, const doubl
 #pragma unroll
             for (int q = 0; q < kBT; q++) {
                 const int e = lane + 64 * q;
-                st[(e >> 4) * kRow + (e & 15)] = nxt[q];
+                if constexpr (IQ16)
+                    st[(e >> 4) * kRow + (e & 15)] =
+                        make_float2(iq16_to_f((short)(nxt[q] & 0xffff)), iq16_to_f((short)(nxt[q] >> 16)));
+                else
+                    st[(e >> 4) * kRow + (e & 15)] = nxt[q];
             }
             if (k + 1 < kBC / kBT) fetch(k + 1);
             iir_wave_sync();
@@ -1071,14 +1096,14 @@ void launch_1p(const Step& st, const float* x, size_t n, const Iir1pPlan& p, con
                        st_out, y);
 }
 
-template <int NC, int D, class Step>
-void launch_blk(const Step& st, const IirDesc& d, const float* x, size_t n, double* state64, const IirBlkPlan& p,
+template <int NC, int D, class Step, bool IQ16 = false>
+void launch_blk(const Step& st, const IirDesc& d, const void* x, size_t n, double* state64, const IirBlkPlan& p,
                 float* y, hipStream_t s)
 {
     const unsigned g = (unsigned)p.nblk;
     {
         LDSP_PROF(s, "k_iir_blk_local");
-        hipLaunchKernelGGL((k_iir_blk<NC, D, false, Step>), dim3(g), dim3(kBN), 0, s, st, x, (long)n, p.nchunks,
+        hipLaunchKernelGGL((k_iir_blk<NC, D, false, Step, IQ16>), dim3(g), dim3(kBN), 0, s, st, x, (long)n, p.nchunks,
                            p.AL, p.local, (const double*)nullptr, p.blocal, (double*)nullptr, (float*)nullptr);
     }
     LDSP_HIP(hipGetLastError());
@@ -1097,14 +1122,14 @@ void launch_blk(const Step& st, const IirDesc& d, const float* x, size_t n, doub
     }
     {
         LDSP_PROF(s, "k_iir_blk_final");
-        hipLaunchKernelGGL((k_iir_blk<NC, D, true, Step>), dim3(g), dim3(kBN), 0, s, st, x, (long)n, p.nchunks,
+        hipLaunchKernelGGL((k_iir_blk<NC, D, true, Step, IQ16>), dim3(g), dim3(kBN), 0, s, st, x, (long)n, p.nchunks,
                            p.AL, p.local, (const double*)p.bstart, (double*)nullptr, state64, y);
     }
     LDSP_HIP(hipGetLastError());
 }
 
-template <int NC, int D>
-void dispatch_blk(const IirDesc& d, const float* cb, const float* ca, const float* x, size_t n, double* state64,
+template <int NC, int D, bool IQ16 = false>
+void dispatch_blk(const IirDesc& d, const float* cb, const float* ca, const void* x, size_t n, double* state64,
                   const IirBlkPlan& p, float* y, hipStream_t s)
 {
     if (d.sos) {
@@ -1115,7 +1140,7 @@ void dispatch_blk(const IirDesc& d, const float* cb, const float* ca, const floa
                     st.b[q][k] = (double)cb[3 * q + k];
                     st.a[q][k] = (double)ca[3 * q + k];
                 }
-            launch_blk<NC, D>(st, d, x, n, state64, p, y, s);
+            launch_blk<NC, D, StepSos<D>, IQ16>(st, d, x, n, state64, p, y, s);
         }
     } else {
         StepTf<D> st;
@@ -1123,7 +1148,7 @@ void dispatch_blk(const IirDesc& d, const float* cb, const float* ca, const floa
             st.b[i] = i < d.nb ? (double)cb[i] : 0.0;
             st.a[i] = i < d.na ? (double)ca[i] : 0.0;
         }
-        launch_blk<NC, D>(st, d, x, n, state64, p, y, s);
+        launch_blk<NC, D, StepTf<D>, IQ16>(st, d, x, n, state64, p, y, s);
     }
 }
 
@@ -1262,16 +1287,17 @@ void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* stat
 namespace ldsp {
 namespace k {
 void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n, double* state64,
-             const IirBlkPlan& p, void* y, hipStream_t s)
+             const IirBlkPlan& p, void* y, hipStream_t s, bool iq16)
 {
     if (n == 0) return;
     LDSP_REQUIRE(d.D >= 1 && d.D <= kIirBlkMaxD, "iir: state dimension too large for the blocked scan");
-    const float* xf = (const float*)x;
+    LDSP_REQUIRE(!iq16 || cplx, "iir: int16 IQ input needs a complex filter");
     float* yf = (float*)y;
 #define LDSP_BLK(DD)                                                                          \
     case DD:                                                                                  \
-        if (cplx) dispatch_blk<2, DD>(d, hb, ha, xf, n, state64, p, yf, s);                    \
-        else dispatch_blk<1, DD>(d, hb, ha, xf, n, state64, p, yf, s);                         \
+        if (iq16) dispatch_blk<2, DD, true>(d, hb, ha, x, n, state64, p, yf, s);               \
+        else if (cplx) dispatch_blk<2, DD>(d, hb, ha, x, n, state64, p, yf, s);                \
+        else dispatch_blk<1, DD>(d, hb, ha, x, n, state64, p, yf, s);                          \
         break;
     switch (d.D) {
         LDSP_BLK(1) LDSP_BLK(2) LDSP_BLK(3) LDSP_BLK(4) LDSP_BLK(5) LDSP_BLK(6) LDSP_BLK(7) LDSP_BLK(8)

@@ -109,8 +109,9 @@ struct IirBlkPlan {
     double* blocal;       // [nblk][ncomp][D]
     double* bstart;       // [nblk][ncomp][D]
 };
+// iq16: x holds int16 (I, Q) pairs, converted on load as bytes_to_iq does
 void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n, double* state64,
-             const IirBlkPlan& p, void* y, hipStream_t s);
+             const IirBlkPlan& p, void* y, hipStream_t s, bool iq16 = false);
 // Single-pass float64 scan (k_iir_1p, D <= 8): blocks of kIir1pBlock samples
 // (32 per thread), each block's start state from the J <= kIir1pJmax blocks
 // before it (decoupled look-back; valid when ||A^(kIir1pBlock J)|| < 2^-70).

@@ -345,6 +345,41 @@ struct IIR {
             return ldsp_iirfilt_execute(q, xi, n, yo, mem, s);
         });
     }
+    // self(bytes_to_iq(raw)) with the conversion fused into the filter's loads
+    // (ldsp_iirfilt_execute_iq16): raw is bytes-like / an int16 or uint8 numpy
+    // array (host; returns numpy complex64) or an int16 / uint8 device tensor
+    // (returns a complex64 device tensor), interleaved int16 (I, Q) pairs.
+    py::object from_bytes(const py::handle& b)
+    {
+        if (!cplx) throw py::value_error("from_bytes: int16 IQ input needs a complex filter");
+        if (is_device_tensor(b)) {
+            py::object& torch = torch_mod();
+            py::object t = py::reinterpret_borrow<py::object>(b).attr("reshape")(-1).attr("contiguous")();
+            py::object dev = t.attr("device");
+            const int tdev = dev.attr("index").cast<int>();
+            if (tdev != torch.attr("cuda").attr("current_device")().cast<int>())
+                throw py::value_error("input tensor is not on the current device");
+            const size_t n = t.attr("numel")().cast<size_t>() * t.attr("element_size")().cast<size_t>() / 4;
+            void* s = reinterpret_cast<void*>(
+                torch.attr("cuda").attr("current_stream")(dev).attr("cuda_stream").cast<uintptr_t>());
+            py::object out = dev_empty(n, true, dev);
+            check(ldsp_iirfilt_execute_iq16(q, tptr(t), n, tptr(out), LDSP_MEM_DEVICE, s));
+            return out;
+        }
+        py::object o = py::reinterpret_borrow<py::object>(b);
+        if (py::isinstance<py::array>(o)) o = py::module_::import("numpy").attr("ascontiguousarray")(o);
+        py::buffer_info bi = py::reinterpret_borrow<py::buffer>(o).request();
+        const size_t n = (size_t)bi.size * (size_t)bi.itemsize / 4;
+        py::array_t<cf> out(n);
+        void* yp = out.mutable_data();
+        int rc;
+        {
+            py::gil_scoped_release rel;
+            rc = ldsp_iirfilt_execute_iq16(q, bi.ptr, n, yp, LDSP_MEM_HOST, nullptr);
+        }
+        check(rc);
+        return std::move(out);
+    }
     bool get_exact() { return exact_; }
     void set_exact(bool e)
     {
@@ -851,6 +886,8 @@ void bind_iir_common(P& c)
     c.def("reset", &C::reset)
         .def("freqresponse", &C::freqresponse)
         .def("__call__", &C::call)
+        .def("from_bytes", &C::from_bytes, py::arg("byts"),
+             "self(bytes_to_iq(byts)) in one pass: int16 (I, Q) pairs converted on load (complex filters)")
         .def_property("exact", &C::get_exact, &C::set_exact)
         .def("sos", &C::sos);
 }
@@ -887,6 +924,8 @@ void bind_proto(py::module_& m, const char* name)
         .def_readonly("As", &C::mAs)
         .def("freqresponse", &C::freqresponse)
         .def("__call__", &C::call)
+        .def("from_bytes", &C::from_bytes, py::arg("byts"),
+             "self(bytes_to_iq(byts)) in one pass: int16 (I, Q) pairs converted on load (complex filters)")
         .def("print", &C::print)
         .def("reset", &C::reset)
         .def_property("exact", &C::get_exact, &C::set_exact)

@@ -38,3 +38,15 @@ def test_tanhf(ora, rng):
     x = np.float32(rng.uniform(-10, 10, 400_000))
     x = np.concatenate([x, np.float32(rng.uniform(-0.7, 0.7, 100_000))])
     assert _ulp_err(ora.math_eval("tanh", x), np.tanh(x.astype(np.float64))) <= 1.5
+
+
+def test_iq16_conversion_sequence_exact():
+    """The fused int16 IQ load (k_iir_blk<IQ16>, iq16_to_f) replaces
+    (float)v / 32767.0f (bytes_to_iq, src/utility.hpp:61-69) by a product and
+    one fma residual correction; it must give the same float for every int16."""
+    import runpy, io, contextlib, os
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        runpy.run_path(os.path.join(os.path.dirname(__file__), "..", "scripts", "analysis", "check_iq16_div.py"),
+                       run_name="__main__")
+    assert buf.getvalue().strip() == "mismatches: 0"
