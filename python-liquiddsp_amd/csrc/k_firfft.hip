@@ -204,18 +204,19 @@ __device__ __forceinline__ float2 nco_mix1(float2 v, long i, const Mix& mx, cons
     return o;
 }
 
-template <int PPL, bool MIX>
+// Raw window loads (the P history samples before the call's start come from
+// hist, which already holds mixed samples).  The NCO mix is applied separately
+// (mix_win) once the data is needed: a mix next to its load would make the wave
+// wait for the load there, which with PREF is before this window's transforms,
+// i.e. no prefetch at all.
+template <int PPL>
 __device__ __forceinline__ void load_win(float2 (&v)[PPL], const float2* __restrict__ x,
-                                         const float2* __restrict__ hist, long n, int halo, long g0, int lane,
-                                         const Mix& mx, const float2* ntab)
+                                         const float2* __restrict__ hist, long n, int halo, long g0, int lane)
 {
     if (g0 >= 0 && g0 + 64 * PPL <= n) {          // interior window: 32-bit lane offsets, no checks
         const float2* __restrict__ xb = x + g0;
 #pragma unroll
         for (int r = 0; r < PPL; r++) v[r] = xb[lane + 64 * r];
-        if (MIX)
-#pragma unroll
-            for (int r = 0; r < PPL; r++) v[r] = nco_mix1(v[r], g0 + lane + 64 * r, mx, ntab);
         return;
     }
 #pragma unroll
@@ -223,14 +224,28 @@ __device__ __forceinline__ void load_win(float2 (&v)[PPL], const float2* __restr
         const long gi = g0 + lane + 64 * r;
         float2 e = make_float2(0.0f, 0.0f);
         if (gi >= 0) {
-            if (gi < n) {
-                e = x[gi];
-                if (MIX) e = nco_mix1(e, gi, mx, ntab);
-            }
+            if (gi < n) e = x[gi];
         } else if (gi >= -halo) {
             e = hist[gi + halo];
         }
         v[r] = e;
+    }
+}
+
+// the NCO mix of the samples of window g0 that come from x (0 <= gi < n)
+template <int PPL>
+__device__ __forceinline__ void mix_win(float2 (&v)[PPL], long n, long g0, int lane, const Mix& mx,
+                                        const float2* ntab)
+{
+    if (g0 >= 0 && g0 + 64 * PPL <= n) {
+#pragma unroll
+        for (int r = 0; r < PPL; r++) v[r] = nco_mix1(v[r], g0 + lane + 64 * r, mx, ntab);
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < PPL; r++) {
+        const long gi = g0 + lane + 64 * r;
+        if (gi >= 0 && gi < n) v[r] = nco_mix1(v[r], gi, mx, ntab);
     }
 }
 
@@ -300,16 +315,18 @@ __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512(const float2* __res
     const long w1 = min(nwin, w0 + per);
     float2* d = buf[wave];
     float2 nx[8];
-    if (PREF && w0 < w1) load_win<8, MIX>(nx, x, hist, n, halo, w0 * M - P, lane, mx, ntab);
+    if (PREF && w0 < w1) load_win<8>(nx, x, hist, n, halo, w0 * M - P, lane);
     for (long w = w0; w < w1; w++) {
         const long g0 = w * M - P;
         float2 v[8];
         if (PREF) {
 #pragma unroll
             for (int r = 0; r < 8; r++) v[r] = nx[r];
-            if (w + 1 < w1) load_win<8, MIX>(nx, x, hist, n, halo, g0 + M, lane, mx, ntab);
+            if (MIX) mix_win<8>(v, n, g0, lane, mx, ntab);
+            if (w + 1 < w1) load_win<8>(nx, x, hist, n, halo, g0 + M, lane);
         } else {
-            load_win<8, MIX>(v, x, hist, n, halo, g0, lane, mx, ntab);
+            load_win<8>(v, x, hist, n, halo, g0, lane);
+            if (MIX) mix_win<8>(v, n, g0, lane, mx, ntab);
         }
         fft512(v, d, ltw, lane);
 #pragma unroll
@@ -353,7 +370,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_fir_fft1024(const float2* __rest
     const long w1 = min(nwin, w0 + per);
     float2* d = buf[wave];
     float2 nx[16];
-    if (PREF && w0 < w1) load_win<16, MIX>(nx, x, hist, n, halo, w0 * M - P, lane, mx, ntab);
+    if (PREF && w0 < w1) load_win<16>(nx, x, hist, n, halo, w0 * M - P, lane);
     for (long w = w0; w < w1; w++) {
         asm volatile("" ::: "memory");    // keep H reads inside the loop (register budget)
         const long g0 = w * M - P;
@@ -361,9 +378,11 @@ __global__ void __launch_bounds__(64 * WAVES) k_fir_fft1024(const float2* __rest
         if (PREF) {
 #pragma unroll
             for (int r = 0; r < 16; r++) v[r] = nx[r];
-            if (w + 1 < w1) load_win<16, MIX>(nx, x, hist, n, halo, g0 + M, lane, mx, ntab);
+            if (MIX) mix_win<16>(v, n, g0, lane, mx, ntab);
+            if (w + 1 < w1) load_win<16>(nx, x, hist, n, halo, g0 + M, lane);
         } else {
-            load_win<16, MIX>(v, x, hist, n, halo, g0, lane, mx, ntab);
+            load_win<16>(v, x, hist, n, halo, g0, lane);
+            if (MIX) mix_win<16>(v, n, g0, lane, mx, ntab);
         }
         fft1024(v, d, ltw, lane);
 #pragma unroll
