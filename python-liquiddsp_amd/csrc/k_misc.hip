@@ -63,26 +63,75 @@ __global__ void __launch_bounds__(256) k_freqdem(const float2* __restrict__ x, c
 
 // ------------------------------------------------------------------ FMStereo loop
 constexpr int kFmChunk = 4096;
+constexpr int kFmBatch = 4;      // samples per speculation batch
+constexpr int kFmCand = 16;      // candidate table indices per sample (64 lanes / kFmBatch)
 
-// Per sample (demod.hpp:61-79; nco_crcf_mix_down with the 1024-entry table):
-//   (r1, i1) = (s + 0j) e^{-j theta};  pe = (float)(0.999 pe + 0.001 atan2(i1, r1))
-//   (r2, i2) = (r1, i1) e^{-j theta};  dtheta += C(alpha pe); theta += C(beta pe) + dtheta
-//   l = s + r2, r = s - r2
-// The chain theta -> index -> atan2 -> pe -> C() -> theta is walked by one
-// lane (~130 dependent instructions per sample).  Evaluating atan2 for the
-// next sample at the 64 indices around the predicted one in the other lanes
-// (the prediction theta + dtheta is within 3 cells here) was measured slower:
-// the compiler cannot interleave the two instruction streams of one wave.
-// Waves 1-3 store chunk c - 1's l / r and stream chunk c + 1 of s into the
-// LDS double buffer while lane 0 walks chunk c.
+// One exact mixer step (demod.hpp:61-79; nco_crcf_mix_down with the 1024-entry
+// table):  (r1, i1) = (x + 0j) e^{-j theta};  pe = (float)(0.999 pe + 0.001 atan2(i1, r1));
+// u = re((r1, i1) e^{-j theta});  dtheta += C(alpha pe);  theta += C(beta pe) + dtheta.
+__device__ __forceinline__ float fm_step(float x, const float* tab, uint32_t& theta, uint32_t& d, float& pe,
+                                         float alpha, float beta)
+{
+    const uint32_t idx = ((theta + (1u << 21)) >> 22) & 0x3ffu;
+    const float sn = tab[idx];
+    const float cs = tab[(idx + 256) & 0x3ffu];
+    const float r1 = x * cs - 0.0f * (-sn);
+    const float i1 = x * (-sn) + 0.0f * cs;
+    pe = (float)(0.999 * (double)pe + 0.001 * (double)lm_atan2f(i1, r1));
+    const float u = r1 * cs - i1 * (-sn);
+    d += lm_constrain(pe * alpha);
+    theta += lm_constrain(pe * beta);
+    theta += d;
+    return u;
+}
+
+// The chain theta -> index -> atan2 -> pe -> C() -> theta is serial and does not
+// coalesce, but atan2 and the mixer output depend only on
+// the input sample and the table index.  So wave 0 runs the chain in batches of
+// kFmBatch samples and, beside batch b (in the same basic block, so the two
+// instruction streams interleave), evaluates atan2 and u for batch b + 1 at
+// kFmCand candidate indices per sample in its 64 lanes: indices around the
+// trajectory extrapolated from the state at batch b's start with the phase error
+// held (theta_h = theta + h (C(beta pe) + d) + C(alpha pe) h (h + 1) / 2).  The
+// chain step then only looks its index up (readlane) -- the same bits the direct
+// evaluation gives.  A batch in which some index falls outside its candidate
+// window (a few per thousand batches on FM composite signals,
+// scripts/analysis: fm_h2) is redone with the direct step from the saved state.
+// Waves 1-3 store chunk c - 1's l / r and stream chunk c + 1 of s into the LDS
+// double buffer while wave 0 walks chunk c.
+struct FmCand {
+    float z, u;          // this lane's atan2 and mixer output
+    uint32_t base;       // first candidate index of this lane's sample
+};
+
+__device__ __forceinline__ FmCand fm_cands(const float* sp, int i0, int cnt, const float* tab, uint32_t theta,
+                                           uint32_t d, float pe, float alpha, float beta, int h0, int lane)
+{
+    const int j = lane / kFmCand;
+    const uint32_t h = (uint32_t)(h0 + j);
+    const uint32_t ca = lm_constrain(pe * alpha), cb = lm_constrain(pe * beta);
+    const uint32_t pred = theta + h * (cb + d) + ca * (h * (h + 1) / 2);
+    FmCand c;
+    c.base = (((pred + (1u << 21)) >> 22) - kFmCand / 2) & 0x3ffu;
+    const uint32_t idx = (c.base + (uint32_t)(lane % kFmCand)) & 0x3ffu;
+    const float x = sp[min(i0 + j, cnt - 1)];   // past the chunk's last batch: a value never used
+    const float sn = tab[idx];
+    const float cs = tab[(idx + 256) & 0x3ffu];
+    const float r1 = x * cs - 0.0f * (-sn);
+    const float i1 = x * (-sn) + 0.0f * cs;
+    c.z = lm_atan2f(i1, r1);
+    c.u = r1 * cs - i1 * (-sn);
+    return c;
+}
+
 __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, long n, FmState* st,
                                                 const float* __restrict__ table, float* __restrict__ lo,
                                                 float* __restrict__ ro)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
-    __shared__ float sb[2][kFmChunk];
-    __shared__ float ub[2][kFmChunk];
+    __shared__ float sb[2][kFmChunk + kFmBatch];
+    __shared__ float ub[2][kFmChunk + 64];     // + 64: lanes 1..63 of wave 0 store their (identical) u here
     const int tid = threadIdx.x;
     for (int i = tid; i < 1024; i += 256) tab[i] = table[i];
     const long nch = (n + kFmChunk - 1) / kFmChunk;
@@ -93,23 +142,53 @@ __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, lon
     __syncthreads();
     for (long c = 0; c <= nch; c++) {
         const int cur = (int)(c & 1);
-        if (tid == 0 && c < nch) {
+        if (tid < 64 && c < nch) {
+            const int lane = tid;
             const long base = c * kFmChunk;
             const int cnt = (int)min((long)kFmChunk, n - base);
             const float* sp = sb[cur];
             float* up = ub[cur];
-            for (int i = 0; i < cnt; i++) {
-                const float x = sp[i];
-                const uint32_t idx = ((theta + (1u << 21)) >> 22) & 0x3ffu;
-                const float sn = tab[idx];
-                const float cs = tab[(idx + 256) & 0x3ffu];
-                const float r1 = x * cs - 0.0f * (-sn);
-                const float i1 = x * (-sn) + 0.0f * cs;
-                pe = (float)(0.999 * (double)pe + 0.001 * (double)lm_atan2f(i1, r1));
-                up[i] = r1 * cs - i1 * (-sn);
-                d += lm_constrain(pe * alpha);
-                theta += lm_constrain(pe * beta);
-                theta += d;
+            const int nb = cnt / kFmBatch;
+            // lane 0 stores the chain's u; the other lanes store the same value past the chunk
+            const int uoff = lane == 0 ? 0 : kFmChunk + lane;
+            FmCand cc{};
+            if (nb > 0) cc = fm_cands(sp, 0, cnt, tab, theta, d, pe, alpha, beta, 0, lane);
+            for (int b = 0; b < nb; b++) {
+                const int i0 = b * kFmBatch;
+                // no branch around it: the candidates share a basic block with the chain steps
+                const FmCand nx = fm_cands(sp, i0 + kFmBatch, cnt, tab, theta, d, pe, alpha, beta, kFmBatch, lane);
+                const uint32_t th0 = theta, d0 = d;
+                const float pe0 = pe;
+                bool miss = false;
+#pragma unroll
+                for (int j = 0; j < kFmBatch; j++) {
+                    const uint32_t idx = ((theta + (1u << 21)) >> 22) & 0x3ffu;
+                    const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)cc.base, j * kFmCand);
+                    const uint32_t off = (idx - bj) & 0x3ffu;
+                    miss |= off >= (uint32_t)kFmCand;
+                    const int ln = __builtin_amdgcn_readfirstlane(j * kFmCand + (int)(off & (kFmCand - 1)));
+                    const float z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.z), ln));
+                    const float u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.u), ln));
+                    pe = (float)(0.999 * (double)pe + 0.001 * (double)z);
+                    up[(i0 + j) * (lane == 0) + uoff] = u;
+                    d += lm_constrain(pe * alpha);
+                    theta += lm_constrain(pe * beta);
+                    theta += d;
+                }
+                if (miss) {      // an index left its window: redo the batch directly
+                    theta = th0;
+                    d = d0;
+                    pe = pe0;
+                    for (int j = 0; j < kFmBatch; j++) {
+                        const float u = fm_step(sp[i0 + j], tab, theta, d, pe, alpha, beta);
+                        up[(i0 + j) * (lane == 0) + uoff] = u;
+                    }
+                }
+                cc = nx;
+            }
+            for (int i = nb * kFmBatch; i < cnt; i++) {
+                const float u = fm_step(sp[i], tab, theta, d, pe, alpha, beta);
+                up[i * (lane == 0) + uoff] = u;
             }
         } else if (tid >= 64) {
             const int nxt = 1 - cur;        // holds chunk c - 1 (results) and receives chunk c + 1
