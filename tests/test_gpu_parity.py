@@ -618,6 +618,20 @@ def test_fmstereo_bitwise(ld, ora, rng, iq_rate, pcm_rate):
     assert_bitwise(g(x[:20_000]), o(x[:20_000]))
 
 
+def test_fmstereo_noise_and_special_operands(ld, ora, rng):
+    """The candidate evaluation (k_fm_pll) on inputs that
+    leave the predicted window often (pure noise) and on exact zeros / repeated
+    samples (the discriminator output s = 0, so atan2 sees signed zeros)."""
+    x = cgauss(rng, 120_000)
+    x[1000:1400] = 0                      # s == 0 over a run
+    x[5000:5300] = x[5000]                # repeated sample: s == 0 again
+    x[7000:7010] = np.complex64(1e-30)    # tiny magnitudes
+    g, o = ld.FMStereo(), ora.FMStereo()
+    y = np.concatenate([g(x[:60_001]), g(x[60_001:])])
+    assert_bitwise(y, o(x))
+    assert g.state() == o.state
+
+
 def test_fmstereo_device_tensor(ld, ora, rng):
     import torch
     x = _fm(rng, 50_000, 600000.0)
