@@ -1956,10 +1956,10 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     c.costas = costas;
     c.alpha_host = q->st.alpha;
     c.y = mbuf;
-    c.scratch = k::pll_parallel(n) ? q->pll[sl].ensure(k::pll_scratch_bytes(n), q->device) : nullptr;
+    c.scratch = k::pll_parallel(n, costas) ? q->pll[sl].ensure(k::pll_scratch_bytes(n), q->device) : nullptr;
     q->last_stats = c.scratch ? (const char*)c.scratch + k::pll_stats_offset(n) : nullptr;
     k::pll_front(c, e.stream);
-    const bool par = k::pll_parallel(n);
+    const bool par = k::pll_parallel(n, costas);
     if (par) q->front.mark(e.stream);     // the sequential loop writes the guess itself: mark after it
     // (A dedicated high-priority walker queue was measured: the ~25 us between
     // walks stayed -- it is the dispatcher waiting for a whole CU to drain for the

@@ -211,7 +211,7 @@ struct PllCall {
 size_t pll_scratch_bytes(size_t n);
 size_t pll_stats_offset(size_t n);     // 4 x u64 walker counters inside the scratch (debug)
 // True when the call runs as candidates + walker (else one sequential loop in pll_back).
-bool pll_parallel(size_t n);
+bool pll_parallel(size_t n, int costas);
 // Front half: the delay-line history for the next call and (parallel calls)
 // the candidate chunks.  Reads only the guess state, never the true state, so
 // it may run while the previous call's pll_back is still walking.

@@ -7,7 +7,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [REPO, os.path.join(REPO, "python-liquiddsp_amd")]
+sys.path[:0] = [REPO, os.environ.get("LDSP_PKG_DIR") or os.path.join(REPO, "python-liquiddsp_amd")]
 import torch  # noqa: E402
 import bench  # noqa: E402
 import liquiddsp as L  # noqa: E402
