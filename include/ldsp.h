@@ -58,7 +58,9 @@ int ldsp_stream_synchronize(void *stream);
 
 /* Test hook: evaluate the loop transcendentals (ldsp_math.hpp) on the device.
  * fn: 0 exp, 1 log, 2 atan2(a, b), 3 tanh, 4 constrain (y as uint32 bits);
- * 5 exp, 6 log through the loops' fast paths (lm_*_loop).
+ * 5 exp, 6 log through the loops' fast paths (lm_*_loop); 7 atan2(a, b) in its
+ * select-only form (lm_atan2f_vsel: the candidate evaluations of k_pll_seqc and
+ * k_fm_pll).
  * a, b, y are device pointers of n floats. */
 int ldsp_debug_math_eval(int fn, const float *a, const float *b, float *y, size_t n, void *stream);
 
@@ -251,6 +253,11 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void *x, size_t n, void *y
  * sample by sample.  All zero after a sequential (short) call.  Synchronises. */
 int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t *entries, uint64_t *repairs,
                              uint64_t *fallbacks);
+/* Diagnostics, no reference counterpart: the carrier-mode short-call loop
+ * (k_pll_seqc, calls below 2 048 samples), cumulative since the object's first
+ * call: candidate batches stepped and batches redone directly because a table
+ * index left its candidate window.  Synchronises. */
+int ldsp_ampmodem_seq_stats(ldsp_ampmodem_t q, uint64_t *batches, uint64_t *redone);
 /* Diagnostics, no reference counterpart: the walker's entry margin B = 2^log2_b
  * for the calls that follow (8..21; 0 restores the default).  A narrower
  * margin leaves fewer entries and fails more gap proofs, so more lane-blocks

@@ -944,7 +944,7 @@ int ldsp_stream_synchronize(void* stream)
 int ldsp_debug_math_eval(int fn, const float* a, const float* b, float* y, size_t n, void* stream)
 {
     return guard([&] {
-        LDSP_REQUIRE(fn >= 0 && fn <= 6, "math_eval: unknown function");
+        LDSP_REQUIRE(fn >= 0 && fn <= 7, "math_eval: unknown function");
         (void)current_device();
         k::math_eval(fn, a, b ? b : a, y, n, (hipStream_t)stream);
     });
@@ -1921,13 +1921,28 @@ int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t* entries, uint64_t* rep
     });
 }
 
+int ldsp_ampmodem_seq_stats(ldsp_ampmodem_t q, uint64_t* batches, uint64_t* redone)
+{
+    return guard([&] {
+        NONNULL(q);
+        k::AmpState st{};
+        if (q->dst.p) {
+            DeviceGuard g(q->device);
+            q->sync_all();
+            LDSP_HIP(hipMemcpy(&st, q->dst.p, sizeof(st), hipMemcpyDeviceToHost));
+        }
+        if (batches) *batches = st.sq_batches;
+        if (redone) *redone = st.sq_redone;
+    });
+}
+
 // Carrier lowpass + delay + PLL walk of AmpModem / BroadcastAM: writes
 // re(v1) / mod_index (costas 0) or the Costas-loop output (costas 1) to mbuf
 // (slot scratch when mbuf is null).  Returns the buffer written.  The caller
 // enqueues its post-filter and then amp_call_end().  Stream order (see AmpObj):
 //   wait slot[s] (call k-2 done with slot s) and front (call k-1's histories and guess)
 //   lowpass, delay history, candidates            -> mark front
-//   wait ord (call k-1's walk and DC blocker)      -> walker
+//   wait ord (call k-1's walk; ord is marked before its DC blocker) -> walker
 // Costas: the candidates start from the true state (the loop's two stable
 // points half a turn apart make a guess ambiguous), so its front also waits for
 // call k-1's walk.

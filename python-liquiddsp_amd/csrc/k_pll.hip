@@ -129,68 +129,6 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
 constexpr int kSqBatch = 4;
 constexpr int kSqCand = 16;
 
-__device__ __forceinline__ float sq_vsel(bool c, float a, float b)
-{
-    float r;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(c);
-    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
-    return r;
-}
-
-// lm_atan2f operation for operation with every select one v_cndmask (no
-// exec-mask regions, so the evaluation interleaves with the chain steps)
-__device__ __forceinline__ float sq_atan2(float y, float x)
-{
-    constexpr float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
-                    pi_lo = -8.7422776573e-08f;
-    constexpr float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
-                    aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
-                    aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
-                    aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
-    const int32_t hx = (int32_t)fbits(x), ix = hx & 0x7fffffff;
-    const int32_t hy = (int32_t)fbits(y), iy = hy & 0x7fffffff;
-    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
-    const int32_t k = (iy - ix) >> 23;
-    const float t = fabs_(y / x);
-    const uint32_t it = fbits(t) & 0x7fffffffu;
-    const bool idm = it < 0x3ee00000u, lt1875 = it < 0x3f980000u, lt0687 = it < 0x3f300000u,
-               lt24375 = it < 0x401c0000u;
-    const float n0 = 2.0f * t - 1.0f, n1 = t - 1.0f, n2 = t - 1.5f;
-    const float d0 = 2.0f + t, d1 = t + 1.0f, d2 = 1.0f + 1.5f * t;
-    float num = sq_vsel(lt1875, sq_vsel(lt0687, n0, n1), sq_vsel(lt24375, n2, -1.0f));
-    float den = sq_vsel(lt1875, sq_vsel(lt0687, d0, d1), sq_vsel(lt24375, d2, t));
-    const float hi = sq_vsel(lt1875, sq_vsel(lt0687, 4.6364760399e-01f, 7.8539812565e-01f),
-                             sq_vsel(lt24375, 9.8279368877e-01f, 1.5707962513e+00f));
-    const float lo = sq_vsel(lt1875, sq_vsel(lt0687, 5.0121582440e-09f, 3.7748947079e-08f),
-                             sq_vsel(lt24375, 3.4473217170e-08f, 7.5497894159e-08f));
-    num = sq_vsel(idm, t, num);
-    den = sq_vsel(idm, 1.0f, den);
-    const float xr = num / den;
-    const float zz = xr * xr;
-    const float w = zz * zz;
-    const float s1 = zz * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
-    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    float z = sq_vsel(idm, xr - xr * (s1 + s2), hi - ((xr * (s1 + s2) - lo) - xr));
-    z = sq_vsel(it < 0x39800000u, t, z);
-    z = sq_vsel(it >= 0x4c800000u, 1.5707962513e+00f + 7.5497894159e-08f, z);
-    z = sq_vsel(it > 0x7f800000u, t + t, z);
-    z = sq_vsel(hx < 0 && k < -26, 0.0f, z);
-    z = sq_vsel(k > 26, pi_o_2 + 0.5f * pi_lo, z);
-    const float zm = z - pi_lo;
-    const float q2 = zm - pi, q1 = pi - zm;
-    const float r = sq_vsel((m & 2) != 0, sq_vsel((m & 1) != 0, q2, q1), sq_vsel((m & 1) != 0, -z, z));
-    const bool spec = iy == 0 || ix == 0 || ix >= 0x7f800000 || iy >= 0x7f800000;
-    const float r_pm2 = sq_vsel(hy < 0, -pi_o_2, pi_o_2);
-    const float r_y0 = sq_vsel(m <= 1, y, sq_vsel(m == 2, pi, -pi));
-    const float r_ii = sq_vsel(m == 0, pi_o_4, sq_vsel(m == 1, -pi_o_4, sq_vsel(m == 2, 3.0f * pi_o_4, -3.0f * pi_o_4)));
-    const float r_ix = sq_vsel(m == 0, 0.0f, sq_vsel(m == 1, -0.0f, sq_vsel(m == 2, pi, -pi)));
-    float rs = sq_vsel(ix == 0x7f800000, sq_vsel(iy == 0x7f800000, r_ii, r_ix), r_pm2);
-    rs = sq_vsel(ix == 0, r_pm2, rs);
-    rs = sq_vsel(iy == 0, r_y0, rs);
-    rs = sq_vsel(ix > 0x7f800000 || iy > 0x7f800000, x + y, rs);
-    return sq_vsel(spec, rs, r);
-}
-
 struct SqCand {
     uint32_t k1, k2, base;
     float out;
@@ -213,7 +151,7 @@ __device__ __forceinline__ SqCand sq_cands(const float2* b0, const float2* b1, i
     const float v0r = u0.x * cs - u0.y * (-sn);
     const float v0i = u0.x * (-sn) + u0.y * cs;
     const float v1r = u1.x * cs - u1.y * (-sn);
-    const float phi = sq_atan2(v0i, v0r);
+    const float phi = lm_atan2f_vsel(v0i, v0r);
     c.k1 = lm_constrain(phi * alpha);
     c.k2 = lm_constrain(phi * beta);
     c.out = v1r / mod_index;
@@ -244,6 +182,7 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
             const int ooff = lane == 0 ? 0 : kSeqChunk + lane;
             const int nb = cnt / kSqBatch;
             SqCand cc{};
+            uint32_t nredo = 0;
             if (nb > 0) cc = sq_cands(b0, b1, 0, cnt, tab, theta, d, k1h, k2h, alpha, beta, in.mod_index, 0, lane);
             for (int b = 0; b < nb; b++) {
                 const int i0 = b * kSqBatch;
@@ -269,6 +208,7 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
                     d = d0;
                     k1h = k1s;
                     k2h = k2s;
+                    nredo++;
                     for (int j = 0; j < kSqBatch; j++) {
                         const Kick k = pll_eval(tab, tidx(theta), b0[i0 + j], b1[i0 + j], alpha, beta, in.mod_index, 0);
                         d += k.k1;
@@ -287,6 +227,10 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
                 k1h = k.k1;
                 k2h = k.k2;
                 ob[i * (lane == 0) + ooff] = k.out;
+            }
+            if (tid == 0) {
+                st->sq_batches += (uint32_t)nb;
+                st->sq_redone += nredo;
             }
         }
         __syncthreads();
@@ -1402,8 +1346,8 @@ void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m
     LDSP_HIP(hipGetLastError());
 }
 
-// Candidates + walk beat the one-lane loop (~0.57 us per sample) from about two
-// thousand samples: their latency is the warm-up plus one recorded chunk
+// Costas mode: candidates + walk beat the one-lane loop (~0.57 us per sample)
+// from kParMin (1 280) samples: their latency is the warm-up plus one recorded chunk
 // (~0.94 ms), then the walk.
 static const size_t kParMin = (size_t)LDSP_KNOB("LDSP_PLL_PARMIN", 1280L);
 // Carrier mode: the candidate-kick sequential loop (k_pll_seqc, ~0.29 us per
@@ -1514,10 +1458,12 @@ void pll_back(const PllCall& c, hipStream_t s)
 {
     if (c.n == 0) return;
     if (!pll_parallel(c.n, c.costas)) {
-        {
+        if (c.costas) {
             LDSP_PROF(s, "k_pll_seq");
-            if (c.costas) hipLaunchKernelGGL(k_pll_seq<true>, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
-            else hipLaunchKernelGGL(k_pll_seqc, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
+            hipLaunchKernelGGL(k_pll_seq<true>, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
+        } else {
+            LDSP_PROF(s, "k_pll_seqc");
+            hipLaunchKernelGGL(k_pll_seqc, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
         }
         LDSP_HIP(hipGetLastError());
         return;

@@ -187,6 +187,8 @@ struct AmpState {         // device-resident PLL state
     uint32_t theta, dtheta;   // true loop state (written by the walker / sequential loop)
     float alpha, beta;
     uint32_t gth[2], gd[2];   // ping-pong guess of the state at the next call's start (candidate end state)
+    uint32_t sq_batches;      // k_pll_seqc diagnostics, cumulative: candidate batches stepped,
+    uint32_t sq_redone;       //   and batches redone with pll_eval (an index left its window)
 };
 // One AmpModem / BroadcastAM PLL call.  x0 = lowpass(x) (precomputed), x1 =
 // delay_m(x) via hist (m samples before x[0]); writes Re(v1)/mod (carrier) or

@@ -133,7 +133,7 @@ struct StreamMark {
 
 // Tuning and diagnostic environment knobs (warm-up lengths, walker margin,
 // debug counters, timeline dumps) are read only by a tuning build
-// (`make TUNING=1`, -DLDSP_TUNING); the product library reads no environment
+// (`make EXTRA=-DLDSP_TUNING`); the product library reads no environment
 // and always uses the default.
 #ifdef LDSP_TUNING
 long knob_env(const char* name, long dflt);

@@ -179,6 +179,80 @@ __host__ __device__ inline float lm_atan2f(float y, float x)
     return spec ? rs : r;
 }
 
+// c ? a : b as one v_cndmask on the device (a ballot of c as the lane mask), a
+// plain select on the host.  The candidate evaluations of the one-wave serial
+// loops (k_pll_seqc, k_fm_pll) call atan2 through lm_atan2f_vsel below: with
+// lm_atan2f's ternaries the compiler forms exec-mask regions, which end the
+// basic block and keep the candidates from interleaving with the chain steps.
+__host__ __device__ inline float vsel(bool c, float a, float b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(c);
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+#else
+    return c ? a : b;
+#endif
+}
+
+// lm_atan2f operation for operation (lm_atanf_pos inlined), every select a
+// vsel.  The same IEEE operations in the same order, so the same bits
+// (ldsp_debug_math_eval fn 7; tests/test_gpu_parity.py::test_device_math_bitwise).
+__host__ __device__ inline float lm_atan2f_vsel(float y, float x)
+{
+    constexpr float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+                    pi_lo = -8.7422776573e-08f;
+    constexpr float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
+                    aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
+                    aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
+                    aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
+    const int32_t hx = (int32_t)fbits(x), ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)fbits(y), iy = hy & 0x7fffffff;
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    const int32_t k = (iy - ix) >> 23;
+    // lm_atanf_pos(|y / x|)
+    const float t = fabs_(y / x);
+    const uint32_t it = fbits(t) & 0x7fffffffu;
+    const bool idm = it < 0x3ee00000u, lt1875 = it < 0x3f980000u, lt0687 = it < 0x3f300000u,
+               lt24375 = it < 0x401c0000u;
+    const float n0 = 2.0f * t - 1.0f, n1 = t - 1.0f, n2 = t - 1.5f;
+    const float d0 = 2.0f + t, d1 = t + 1.0f, d2 = 1.0f + 1.5f * t;
+    float num = vsel(lt1875, vsel(lt0687, n0, n1), vsel(lt24375, n2, -1.0f));
+    float den = vsel(lt1875, vsel(lt0687, d0, d1), vsel(lt24375, d2, t));
+    const float hi = vsel(lt1875, vsel(lt0687, 4.6364760399e-01f, 7.8539812565e-01f),
+                          vsel(lt24375, 9.8279368877e-01f, 1.5707962513e+00f));
+    const float lo = vsel(lt1875, vsel(lt0687, 5.0121582440e-09f, 3.7748947079e-08f),
+                          vsel(lt24375, 3.4473217170e-08f, 7.5497894159e-08f));
+    num = vsel(idm, t, num);
+    den = vsel(idm, 1.0f, den);
+    const float xr = num / den;
+    const float zz = xr * xr;
+    const float w = zz * zz;
+    const float s1 = zz * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    float z = vsel(idm, xr - xr * (s1 + s2), hi - ((xr * (s1 + s2) - lo) - xr));
+    z = vsel(it < 0x39800000u, t, z);
+    z = vsel(it >= 0x4c800000u, 1.5707962513e+00f + 7.5497894159e-08f, z);
+    z = vsel(it > 0x7f800000u, t + t, z);
+    // lm_atan2f after the atan
+    z = vsel(hx < 0 && k < -26, 0.0f, z);
+    z = vsel(k > 26, pi_o_2 + 0.5f * pi_lo, z);
+    const float zm = z - pi_lo;
+    const float q2 = zm - pi, q1 = pi - zm;
+    const float r = vsel((m & 2) != 0, vsel((m & 1) != 0, q2, q1), vsel((m & 1) != 0, -z, z));
+    const bool spec = iy == 0 || ix == 0 || ix >= 0x7f800000 || iy >= 0x7f800000;
+    const float r_pm2 = vsel(hy < 0, -pi_o_2, pi_o_2);
+    const float r_y0 = vsel(m <= 1, y, vsel(m == 2, pi, -pi));
+    const float r_ii = vsel(m == 0, pi_o_4, vsel(m == 1, -pi_o_4, vsel(m == 2, 3.0f * pi_o_4, -3.0f * pi_o_4)));
+    const float r_ix = vsel(m == 0, 0.0f, vsel(m == 1, -0.0f, vsel(m == 2, pi, -pi)));
+    float rs = vsel(ix == 0x7f800000, vsel(iy == 0x7f800000, r_ii, r_ix), r_pm2);
+    rs = vsel(ix == 0, r_pm2, rs);
+    rs = vsel(iy == 0, r_y0, rs);
+    rs = vsel(ix > 0x7f800000 || iy > 0x7f800000, x + y, rs);
+    return vsel(spec, rs, r);
+}
+
 // tanh: odd minimax polynomial below 0.625, 1 - 2/(e^{2|x|}+1) above
 __host__ __device__ inline float lm_tanhf(float x)
 {

@@ -662,6 +662,12 @@ struct AmpModem {
         check(ldsp_ampmodem_walk_stats(q, &e, &r, &f));
         return py::make_tuple(e, r, f);
     }
+    py::tuple seq_stats()
+    {
+        uint64_t b, r;
+        check(ldsp_ampmodem_seq_stats(q, &b, &r));
+        return py::make_tuple(b, r);
+    }
     py::object demod(const py::handle& x)
     {
         return run_same(x, true, false, [&](const void* xi, size_t n, void* yo, int mem, void* s) {
@@ -1019,6 +1025,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("reset", &AmpModem::reset)
         .def("pll_state", &AmpModem::pll_state)
         .def("_walk_stats", &AmpModem::walk_stats)
+        .def("_seq_stats", &AmpModem::seq_stats)
         .def("__call__", &AmpModem::demod);
 
     // ---- NCO (wrapper.cpp:201-212)

@@ -113,3 +113,42 @@ def test_resampler_config2_full_size(ld, ora):
     ref = ora.Resampler(np.float32(48000 / 2000000), 20, np.float32(48000 / 2000000), 60.0, 13)(xd.cpu().numpy())
     assert y.shape == ref.shape == (1610613,)
     assert np.array_equal(bits(y), bits(ref))
+
+
+def test_mix_filter_config3_full_size_vs_oracle(ld, ora):
+    """BASELINE config 3 at its full size: NCO.mix_down -> 255-tap ComplexFIRFilter
+    on 256 Mi samples in one call (reference src/nco.hpp:74-80 then
+    src/firfilter.hpp:29-35).  Fused == unfused bit for bit over the whole
+    stream, and within SURVEY 8(d)'s 1e-6 of the restatement on a 1 Mi prefix
+    and on a 1 Mi window at the end (the restatement's NCO advanced to the
+    window's start, its FIR fed the 254 samples before it)."""
+    import torch
+    n, w, L = 256 << 20, 1 << 20, 255
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    xd = torch.complex(torch.randn(n, generator=g, device="cuda"), torch.randn(n, generator=g, device="cuda"))
+    h = ora.firdes_kaiser(L, 0.05, 60.0)
+    freq = np.float32(2 * np.pi * 0.05)
+    out = []
+    for fused in (True, False):
+        nco = ld.NCO("nco")
+        nco.freq = freq
+        f = ld.ComplexFIRFilter(h)
+        out.append(ld.mix_down_filter(nco, f, xd) if fused else f(nco.mix_down(xd)))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0].view(torch.float32), out[1].view(torch.float32))
+    y = out[0]
+    del out[1]
+    # prefix
+    on = ora.NCO(0)
+    on.freq = freq
+    dtheta = on.state[1]
+    ref = ora.FIRFilter(h, cplx=True)(on.mix_down(xd[:w].cpu().numpy()))
+    assert maxrel(y[:w].cpu().numpy(), ref) <= 1e-6
+    # tail window [n - w, n): restatement started L - 1 samples early
+    a = n - w - (L - 1)
+    on = ora.NCO(0)
+    on.freq = freq
+    on.state = ((a * dtheta) & 0xFFFFFFFF, dtheta)
+    ref = ora.FIRFilter(h, cplx=True)(on.mix_down(xd[a:].cpu().numpy()))[L - 1:]
+    assert maxrel(y[n - w:].cpu().numpy(), ref) <= 1e-6

@@ -60,13 +60,16 @@ def test_device_math_bitwise(ld, ora, rng):
         ta = torch.from_numpy(a).cuda()
         tb = torch.from_numpy(b if b is not None else a).cuda()
         ty = torch.empty_like(ta)
-        ld._math_eval(fn, ta.data_ptr(), tb.data_ptr(), ty.data_ptr(), a.size, 0)
-        torch.cuda.synchronize()
-        got, ref = ty.cpu().numpy(), ora.math_eval(names[fn], a, b)
-        if key == 5:                      # NaN payloads are not specified: NaN-ness only
-            assert np.array_equal(np.isnan(got), np.isnan(ref))
-            got, ref = got[~np.isnan(ref)], ref[~np.isnan(ref)]
-        assert_bitwise(got, ref)
+        # atan2 twice: lm_atan2f (fn 2) and its select-only form lm_atan2f_vsel
+        # (fn 7, the candidate evaluations of k_pll_seqc and k_fm_pll)
+        for f in ((2, 7) if fn == 2 else (fn,)):
+            ld._math_eval(f, ta.data_ptr(), tb.data_ptr(), ty.data_ptr(), a.size, 0)
+            torch.cuda.synchronize()
+            got, ref = ty.cpu().numpy(), ora.math_eval(names[fn], a, b)
+            if key == 5:                      # NaN payloads are not specified: NaN-ness only
+                assert np.array_equal(np.isnan(got), np.isnan(ref))
+                got, ref = got[~np.isnan(ref)], ref[~np.isnan(ref)]
+            assert_bitwise(got, ref)
     # the AGC loop's fast paths (fn 5 exp, 6 log: lm_*_loop, scaling-free division
     # on the device) must give the general functions' bits everywhere, in and out
     # of their fast ranges

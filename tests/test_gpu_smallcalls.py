@@ -2,11 +2,13 @@
 65 536 IQ samples per call -> ~1 573 PCM samples through the AGC and the AmpModem.
 
 At that size the AGC runs its chunks from the true state with the approximate
-loop up to each chunk (k_agc_chunks, tsa mode) and the AmpModem PLL runs
-candidates + walk (k_pll_cand from 1 280 samples); both must stay bit-identical
-to the sequential restatement, including the calls whose approximate trajectory
-left the exact one (re-run by k_agc_runfix / k_agc_verify), and across calls
-rotating over several streams.
+loop up to each chunk (k_agc_chunks, tsa mode) and the carrier-mode AmpModem
+PLL runs the one-wave candidate-kick loop (k_pll_seqc, below 2 048 samples;
+its own tests are in test_gpu_pll_seqc.py; Costas mode runs candidates + walk
+from 1 280 samples); both must stay bit-identical to the sequential
+restatement, including the calls whose approximate trajectory left the exact
+one (re-run by k_agc_runfix / k_agc_verify), and across calls rotating over
+several streams.
 """
 import numpy as np
 import pytest
