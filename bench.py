@@ -330,7 +330,7 @@ def main():
     # its output once; complex64 = 8 B, float32 = 4 B).  Multi-kernel stages
     # attribute the stage minimum to the kernel that produces the stage output.
     n = args.n
-    alg = {"k_iir_scan_local": 8 * n, "k_iir_scan_carry": 0, "k_iir_scan_final": 16 * n,
+    alg = {"k_iir_modal": 16 * n, "k_iir_scan_local": 8 * n, "k_iir_scan_carry": 0, "k_iir_scan_final": 16 * n,
            "k_iir_blk_local": 8 * n, "k_iir_blk_final": 16 * n,
            "k_resamp": 8 * n + 8 * n_pcm, "k_agc_chunks": 16 * n_pcm, "k_agc_verify": 0,
            "k_fir_exact": 8 * n_pcm + 8 * n_pcm, "k_pll_cand": 12 * n_pcm, "k_pll_walk": 12 * n_pcm,
@@ -365,16 +365,7 @@ def main():
                    "carrier_hz": CARRIERS[(rank if args.channel is None else args.channel) % len(CARRIERS)],
                    "seed": 4 if (rank if args.channel is None else args.channel) == 0 else 10 + (rank if args.channel is None else args.channel),
                    "parallelism": f"channel-per-gpu x{world}" + (" rank0-scatter/gather" if args.scatter and dist else "")},
-        "roofline": {"bound": "hbm", "kernel": dom, "ms_per_launch": round(dom_ms, 4),
-                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("bench", dom),
-                     "traffic_source": PMC_SOURCE,
-                     "note": "alg bytes = 12 B per PCM sample (AmpModem in + out); the PLL recurrence is "
-                             "latency-bound (one serial walker wave), not HBM-bound" if dom == "k_pll_walk" else "",
-                     "serial_chain": {"entries": int(entries), "repairs": int(repairs), "fallback_lane_blocks": int(fallbacks),
-                                      "floor_ns_per_repair": REPAIR_FLOOR_NS,
-                                      "floor_ms": round(repairs * REPAIR_FLOOR_NS * 1e-6, 4),
-                                      "frac": round(repairs * REPAIR_FLOOR_NS * 1e-6 / dom_ms, 3) if dom_ms else None}},
+        "roofline": roofline(dom, dom_ms, achieved, entries, repairs, fallbacks),
         "streams": nstreams,
         "host_ms_per_step": round(host_ms, 4),
         "host_ms_max_step": round(host_max_ms, 4),
@@ -392,6 +383,31 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def roofline(dom, dom_ms, achieved, entries, repairs, fallbacks):
+    """The dominant kernel against the roof that bounds it.  The PLL walk is one
+    serial chain of dependent repairs: its roof is the
+    measured per-repair floor (scripts/ubench/walk_loop.hip), so the primary
+    figures are repairs per ms against that floor; its HBM view is kept beside
+    (12 B per PCM sample, a tiny fraction by construction)."""
+    hbm = {"bound": "hbm", "kernel": dom, "ms_per_launch": round(dom_ms, 4), "achieved": round(achieved, 2),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+           "traffic": pmc_traffic("bench", dom), "traffic_source": PMC_SOURCE}
+    if dom != "k_pll_walk":
+        return hbm
+    peak = 1e6 / REPAIR_FLOOR_NS                        # dependent repairs per ms at the floor
+    ach = repairs / dom_ms if dom_ms else 0.0
+    return {"bound": "serial", "kernel": dom, "ms_per_launch": round(dom_ms, 4),
+            "achieved": round(ach, 1), "peak": round(peak, 1), "unit": "dependent repairs/ms",
+            "frac": round(ach / peak, 3) if peak else None,
+            "traffic": hbm["traffic"], "traffic_source": PMC_SOURCE,
+            "serial_chain": {"entries": int(entries), "repairs": int(repairs), "fallback_lane_blocks": int(fallbacks),
+                             "floor_ns_per_repair": REPAIR_FLOOR_NS,
+                             "floor_ms": round(repairs * REPAIR_FLOOR_NS * 1e-6, 4)},
+            "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac")},
+            "note": "the PLL recurrence is one serial walker wave: bounded by the dependent-repair latency "
+                    "(floor_ns_per_repair), not by HBM (alg bytes 12 B per PCM sample)"}
 
 
 def _pmc_summary():

@@ -177,8 +177,10 @@ int ldsp_nco_mix_firfilt(ldsp_nco_t nco, ldsp_firfilt_t fir, const void *x, size
  * ftype: 0 butter 1 cheby1 2 cheby2 3 ellip 4 bessel;
  * btype: 0 lowpass 1 highpass 2 bandpass 3 bandstop.
  * Mode FAST evaluates the cascade as a chunked linear scan in float64 (more
- * accurate than liquid's float32 recursion); EXACT runs the float32 direct-form
- * II recursion sequentially (bit-identical to the restatement).
+ * accurate than liquid's float32 recursion): in one pass over memory in the
+ * filter's modal coordinates when they are well-conditioned, else as a blocked
+ * scan of the SOS state; EXACT runs the float32 direct-form II recursion
+ * sequentially (bit-identical to the restatement).
  * ---------------------------------------------------------------------- */
 typedef struct ldsp_iirfilt_s *ldsp_iirfilt_t;
 int ldsp_iirfilt_create_prototype(int ftype, int btype, unsigned int order, float fc, float f0,
@@ -187,6 +189,17 @@ int ldsp_iirfilt_create_sos(const float *B, const float *A, unsigned int nsos, i
                             ldsp_iirfilt_t *q);
 int ldsp_iirfilt_create_tf(const float *b, unsigned int nb, const float *a, unsigned int na, int cplx,
                            ldsp_iirfilt_t *q);
+/* Test / diagnostic hooks for the fast-mode evaluation.  The fast mode runs the
+ * single-pass modal scan (k_iir_modal) when the filter's modal form passed its
+ * host check at creation (ok = 1: modes M, look-back depth J in 2048-sample
+ * units, check error err), else the blocked SOS-coordinate scan.  path: 0
+ * automatic, 1 force the blocked scan, 2 require the modal scan (LDSP_EINVAL
+ * when the filter has none), 3 the modal scan with every look-back recomputed
+ * from the input (the path a wave takes when a predecessor is late).  A forced
+ * path also replaces the speculative exact path of fast-decaying filters;
+ * exact mode is unaffected. */
+int ldsp_debug_iir_path(ldsp_iirfilt_t q, int path);
+int ldsp_debug_iir_modal_info(ldsp_iirfilt_t q, int *ok, int *modes, int *lookback, double *err);
 int ldsp_iirfilt_destroy(ldsp_iirfilt_t q);
 int ldsp_iirfilt_reset(ldsp_iirfilt_t q);
 int ldsp_iirfilt_set_mode(ldsp_iirfilt_t q, int mode);

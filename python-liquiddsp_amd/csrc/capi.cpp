@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "design.hpp"
+#include "modal.hpp"
 #include "kernels.hpp"
 #include "ldsp_math.hpp"
 #include "ldsp_common.hpp"
@@ -320,17 +321,18 @@ struct IirObj {
     DevBuf db, da, st32, st64, sc1, sc2, mats;
     DevBuf bmats, bsc1, bsc2, bsc3;   // blocked scan (D <= 8): matrices and scratch
     int bplan_G = 0;
-    // single-pass scan (k_iir_1p): look-back depth (0: the filter decays too
-    // slowly, use the blocked scan), tables, per-block aggregates and flags,
-    // the ticket counter, the call epoch, and the second state buffer (the
-    // kernel reads the call's start state from st64 and writes the end state
-    // into st64b; the two are swapped after the call)
-    int J1p = 0;
-    DevBuf p1mats, p1agg, p1flags, p1ticket, st64b;
+    // single-pass modal scan (k_iir_modal.hip): the modal form (ok == false:
+    // the blocked scan), its tables, the per-unit published end states, the
+    // call epoch, and the modal state in two buffers (a call reads its start
+    // state from mst and writes its end state into mstb; swapped after the call)
+    ModalForm mf;
+    DevBuf mtab, magg, mst, mstb;
+    long magg_units = 0;
+    uint32_t m_epoch = 0;
+    int path_force = 0;               // ldsp_debug_iir_path: 0 auto, 1 blocked scan, 2 modal
     DevBuf iq;                        // int16 IQ converted for the paths that do not read it themselves
-    long p1_nblk_cap = 0;
-    unsigned p1_epoch = 0;
-    bool state_in64 = false;          // where the authoritative state lives
+    enum { kSt32 = 0, kSt64 = 1, kStModal = 2 };
+    int state_at = kSt32;             // where the authoritative state lives
     int plan_C = 0;
     long plan_nch = 0;
     int plan_G = 0;
@@ -342,28 +344,31 @@ struct IirObj {
     int fsz() const { return sos ? 3 * (int)nsos : nv; }
     int ncomp() const { return cplx ? 2 : 1; }
 
-    // float64 step on a state vector (same layout as the scan kernels)
-    double step_host(std::vector<double>& v, double x) const
+    // one step of the recursion on a state vector (the layout of the scan
+    // kernels), in double or long double
+    template <class R>
+    R step_t(std::vector<R>& v, R x) const
     {
         if (sos) {
-            double t = x;
+            R t = x;
             for (unsigned s = 0; s < nsos; s++) {
-                const double v1 = v[2 * s], v2 = v[2 * s + 1];
-                const double v0 = t - (double)a[3 * s + 1] * v1 - (double)a[3 * s + 2] * v2;
-                t = (double)b[3 * s] * v0 + (double)b[3 * s + 1] * v1 + (double)b[3 * s + 2] * v2;
+                const R v1 = v[2 * s], v2 = v[2 * s + 1];
+                const R v0 = t - (R)a[3 * s + 1] * v1 - (R)a[3 * s + 2] * v2;
+                t = (R)b[3 * s] * v0 + (R)b[3 * s + 1] * v1 + (R)b[3 * s + 2] * v2;
                 v[2 * s + 1] = v1;
                 v[2 * s] = v0;
             }
             return t;
         }
-        double r = x;
-        for (int i = 1; i < na; i++) r -= (double)a[i] * v[i - 1];
-        double y = (double)b[0] * r;
-        for (int i = 1; i < nb; i++) y += (double)b[i] * v[i - 1];
+        R r = x;
+        for (int i = 1; i < na; i++) r -= (R)a[i] * v[i - 1];
+        R y = (R)b[0] * r;
+        for (int i = 1; i < nb; i++) y += (R)b[i] * v[i - 1];
         for (int i = D - 1; i > 0; i--) v[i] = v[i - 1];
         if (D > 0) v[0] = r;
         return y;
     }
+    double step_host(std::vector<double>& v, double x) const { return step_t<double>(v, x); }
 
     void finalize()
     {
@@ -375,24 +380,21 @@ struct IirObj {
             step_host(v, 0.0);
             for (int r = 0; r < D; r++) A[(size_t)r * D + c] = v[r];
         }
-        // single-pass scan: smallest J with ||A^(kIir1pBlock J)||_inf < 2^-70
-        J1p = 0;
-        if (D > 0 && D <= k::kIirBlkMaxD) {
-            const std::vector<double> AB = matpow(A, (uint64_t)k::kIir1pBlock);
-            std::vector<double> P = AB;
-            for (int j = 1; j <= k::kIir1pJmax; j++) {
-                double nrm = 0;
-                for (int r = 0; r < D; r++) {
-                    double sum = 0;
-                    for (int q = 0; q < D; q++) sum += fabs(P[(size_t)r * D + q]);
-                    nrm = std::max(nrm, sum);
-                }
-                if (nrm < 8.5e-22) {
-                    J1p = j;
-                    break;
-                }
-                P = matmul(P, AB);
+        // modal form for the single-pass scan (long-double state space)
+        mf = ModalForm{};
+        if (D > 0) {
+            using L = long double;
+            std::vector<L> Al((size_t)D * D), Bl(D), Cl(D);
+            for (int c = 0; c < D; c++) {
+                std::vector<L> v(D, 0.0L);
+                v[c] = 1.0L;
+                Cl[c] = step_t<L>(v, 0.0L);
+                for (int r = 0; r < D; r++) Al[(size_t)r * D + c] = v[r];
             }
+            std::vector<L> v(D, 0.0L);
+            const L Dd = step_t<L>(v, 1.0L);
+            Bl = v;
+            mf = modal_form(D, Al, Bl, Cl, Dd, sos ? sos_poles(a, nsos) : tf_poles(a, na, D));
         }
         // decay length: smallest 2^k with ||A^(2^k)||_inf < 2^-70
         spec_W = 0;
@@ -444,8 +446,13 @@ struct IirObj {
         zero_now(st32.p, 0, sizeof(float) * 2 * std::max(fsz(), 1));
         st64.ensure(sizeof(double) * 2 * std::max(D, 1), dev);
         zero_now(st64.p, 0, sizeof(double) * 2 * std::max(D, 1));
-        st64b.ensure(sizeof(double) * 2 * std::max(D, 1), dev);
-        state_in64 = false;
+        if (mf.ok) {
+            const size_t mb = sizeof(double) * 2 * 2 * mf.M;
+            zero_now(mst.ensure(mb, dev), 0, mb);
+            mstb.ensure(mb, dev);
+            upload(mtab, mf.tables, dev);
+        }
+        state_at = kSt32;
         device = dev;
     }
     k::IirDesc desc() const
@@ -461,15 +468,18 @@ struct IirObj {
         d.a = da.as<float>();
         return d;
     }
-    // move the authoritative state between the float32 and float64 layouts
-    void state_to(bool to64, hipStream_t s)
+    // Move the authoritative state between the float32 DF-II layout (exact
+    // paths), the float64 layout of the SOS-coordinate scans and the modal
+    // coordinates (k_iir_modal), through the host (mode switches only).
+    void state_to(int to, hipStream_t s)
     {
-        if (state_in64 == to64) return;
+        if (state_at == to) return;
         const int nc = ncomp(), fs = fsz();
-        std::vector<float> f(2 * std::max(fs, 1), 0.0f);
         std::vector<double> d(2 * std::max(D, 1), 0.0);
         LDSP_HIP(hipStreamSynchronize(s));
-        if (to64) {
+        // 1. current state -> float64 layout d
+        if (state_at == kSt32) {
+            std::vector<float> f(2 * std::max(fs, 1), 0.0f);
             LDSP_HIP(hipMemcpy(f.data(), st32.p, f.size() * 4, hipMemcpyDeviceToHost));
             for (int c = 0; c < nc; c++) {
                 if (sos)
@@ -480,9 +490,24 @@ struct IirObj {
                 else
                     for (int i = 0; i < D; i++) d[c * D + i] = f[c * fs + i];
             }
-            LDSP_HIP(hipMemcpy(st64.p, d.data(), d.size() * 8, hipMemcpyHostToDevice));
-        } else {
+        } else if (state_at == kSt64) {
             LDSP_HIP(hipMemcpy(d.data(), st64.p, d.size() * 8, hipMemcpyDeviceToHost));
+        } else {
+            const int M = mf.M;
+            std::vector<double> z(2 * 2 * M);
+            LDSP_HIP(hipMemcpy(z.data(), mst.p, z.size() * 8, hipMemcpyDeviceToHost));
+            for (int c = 0; c < nc; c++)
+                for (int i = 0; i < D; i++) {
+                    double v = 0;
+                    for (int m = 0; m < M; m++)
+                        v += (mf.to_s[(size_t)i * M + m] *
+                              std::complex<double>(z[(c * M + m) * 2], z[(c * M + m) * 2 + 1])).real();
+                    d[c * D + i] = v;
+                }
+        }
+        // 2. float64 layout -> target
+        if (to == kSt32) {
+            std::vector<float> f(2 * std::max(fs, 1), 0.0f);
             for (int c = 0; c < nc; c++) {
                 if (sos)
                     for (unsigned q = 0; q < nsos; q++) {
@@ -494,8 +519,21 @@ struct IirObj {
                     for (int i = 0; i < fs; i++) f[c * fs + i] = i < D ? (float)d[c * D + i] : 0.0f;
             }
             LDSP_HIP(hipMemcpy(st32.p, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+        } else if (to == kSt64) {
+            LDSP_HIP(hipMemcpy(st64.p, d.data(), d.size() * 8, hipMemcpyHostToDevice));
+        } else {
+            const int M = mf.M;
+            std::vector<double> z(2 * 2 * M, 0.0);
+            for (int c = 0; c < nc; c++)
+                for (int m = 0; m < M; m++) {
+                    std::complex<double> v = 0;
+                    for (int i = 0; i < D; i++) v += mf.to_z[(size_t)m * D + i] * d[c * D + i];
+                    z[(c * M + m) * 2] = v.real();
+                    z[(c * M + m) * 2 + 1] = v.imag();
+                }
+            LDSP_HIP(hipMemcpy(mst.p, z.data(), z.size() * 8, hipMemcpyHostToDevice));
         }
-        state_in64 = to64;
+        state_at = to;
     }
     // Blocked scan plan (k_iir_blk): 256-sample chunks, 256 chunks per block.
     k::IirBlkPlan blk_plan(size_t n)
@@ -534,45 +572,30 @@ struct IirObj {
         p.bstart = (double*)bsc3.ensure((size_t)nblk * ncomp() * D * sizeof(double), device);
         return p;
     }
-    k::Iir1pPlan one_pass_plan(size_t n)
+    // Modal scan plan: the tables (uploaded with the state), the per-unit
+    // granules (zero when allocated: below every epoch) and this call's epoch.
+    k::IirModalPlan modal_plan(size_t n)
     {
-        const size_t DD = (size_t)D * D;
-        if (!p1mats.p) {
-            std::vector<double> all;
-            const std::vector<double> A32 = matpow(A, 32);
-            std::vector<double> M = matpow(A, 0);
-            for (int j = 0; j < 256; j++) {           // A^{32 j}
-                all.insert(all.end(), M.begin(), M.end());
-                M = matmul(M, A32);
-            }
-            const std::vector<double> AB = matpow(A, (uint64_t)k::kIir1pBlock);
-            M = matpow(A, 0);
-            for (int j = 0; j < J1p; j++) {           // A^{kIir1pBlock j}
-                all.insert(all.end(), M.begin(), M.end());
-                M = matmul(M, AB);
-            }
-            upload(p1mats, all, device);
-            p1ticket.ensure(64, device);
-            zero_now(p1ticket.p, 0, 64);
+        const long units = k::iir_modal_units(n);
+        const size_t per = (size_t)ncomp() * mf.M * 4 * sizeof(uint64_t);
+        if (units > magg_units) {
+            magg.ensure((size_t)units * per, device);
+            zero_now(magg.p, 0, magg.cap);
+            magg_units = (long)(magg.cap / per);
         }
-        const long nblk = (long)((n + k::kIir1pBlock - 1) / k::kIir1pBlock);
-        if (nblk > p1_nblk_cap) {                     // flags start at 0 (< every epoch)
-            p1flags.ensure((size_t)nblk * 4, device);
-            zero_now(p1flags.p, 0, p1flags.cap);
-            p1_nblk_cap = (long)(p1flags.cap / 4);
+        if (++m_epoch == 0) {                         // wrapped: restart the granules
+            zero_now(magg.p, 0, magg.cap);
+            m_epoch = 1;
         }
-        k::Iir1pPlan p;
-        p.J = J1p;
-        p.AC = p1mats.as<double>();
-        p.AB = p.AC + 256 * DD;
-        p.agg = (double*)p1agg.ensure((size_t)nblk * ncomp() * D * sizeof(double), device);
-        p.flags = p1flags.as<unsigned>();
-        p.ticket = p1ticket.as<unsigned>();
-        if (++p1_epoch == 0) {                        // wrapped: restart the flags
-            zero_now(p1flags.p, 0, p1flags.cap);
-            p1_epoch = 1;
-        }
-        p.epoch = p1_epoch;
+        k::IirModalPlan p;
+        p.J = mf.J;
+        p.PS = mtab.as<double>();
+        p.PL = p.PS + 6 * mf.M * 2;
+        p.PB = p.PL + 64 * mf.M * 2;
+        p.agg = magg.as<uint64_t>();
+        p.epoch = m_epoch;
+        p.recompute = path_force == 3 ? 1 : 0;
+        p.variant = LDSP_KNOB("LDSP_IIR_VARIANT", 0);
         return p;
     }
     k::IirScanPlan scan_plan(size_t n)
@@ -1470,6 +1493,7 @@ int ldsp_iirfilt_reset(ldsp_iirfilt_t q)
         DeviceGuard g(q->device);
         LDSP_HIP(hipMemsetAsync(q->st32.p, 0, q->st32.cap, q->last));
         LDSP_HIP(hipMemsetAsync(q->st64.p, 0, q->st64.cap, q->last));
+        if (q->mst.p) LDSP_HIP(hipMemsetAsync(q->mst.p, 0, q->mst.cap, q->last));
         q->ord.mark(q->last);              // a call on another stream waits for the zeroing
     });
 }
@@ -1485,6 +1509,26 @@ int ldsp_iirfilt_set_mode(ldsp_iirfilt_t q, int mode)
 int ldsp_iirfilt_get_nsos(ldsp_iirfilt_t q, unsigned int* n)
 {
     return guard([&] { NONNULL(q); NONNULL(n); *n = q->sos ? q->nsos : 0; });
+}
+int ldsp_debug_iir_path(ldsp_iirfilt_t q, int path)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(path >= 0 && path <= 3,
+                     "iirfilt: path must be 0 (automatic), 1 (blocked scan), 2 (modal) or 3 (modal, look-back recomputed)");
+        LDSP_REQUIRE(path < 2 || q->mf.ok, "iirfilt: this filter has no valid modal form");
+        q->path_force = path;
+    });
+}
+int ldsp_debug_iir_modal_info(ldsp_iirfilt_t q, int* ok, int* modes, int* lookback, double* err)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (ok) *ok = q->mf.ok ? 1 : 0;
+        if (modes) *modes = q->mf.M;
+        if (lookback) *lookback = q->mf.J;
+        if (err) *err = q->mf.err;
+    });
 }
 int ldsp_iirfilt_get_sos(ldsp_iirfilt_t q, float* B, float* A)
 {
@@ -1543,18 +1587,21 @@ static int iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, i
         void* dy = q->stg.dev_out(e, y, bytes);
         if (n > 0) {
             const k::IirDesc d = q->desc();
-            const bool blk = !(q->spec_W > 0 && q->spec_W <= 16384) && q->mode != LDSP_MODE_EXACT &&
-                             !(q->J1p > 0 && LDSP_KNOB("LDSP_IIR_1P", 0)) && q->D <= k::kIirBlkMaxD &&
-                             !LDSP_KNOB("LDSP_IIR_OLDSCAN", 0);
-            if (iq16 && !blk) {                    // not fused: convert first
+            enum { kSpec, kSeq, kModal, kBlk, kScan } path;
+            if (q->mode == LDSP_MODE_EXACT || q->D == 0) path = kSeq;
+            else if (q->path_force == 0 && q->spec_W > 0 && q->spec_W <= 16384) path = kSpec;   // fast-decaying: exact chunks
+            else if (q->mf.ok && q->path_force != 1) path = kModal;
+            else if (q->D <= k::kIirBlkMaxD) path = kBlk;
+            else path = kScan;
+            if (iq16 && path != kModal && path != kBlk) {   // not fused: convert first
                 void* cx = q->iq.ensure(n * 8, q->device);
                 k::bytes_to_iq(dx, cx, n, e.stream);
                 dx = cx;
                 iq16 = false;
             }
-            if (q->spec_W > 0 && q->spec_W <= 16384) {
-                // fast-decaying filter: speculative exact chunks (same bits as sequential)
-                q->state_to(false, e.stream);
+            switch (path) {
+            case kSpec: {   // speculative exact chunks (same bits as sequential)
+                q->state_to(IirObj::kSt32, e.stream);
                 k::SpecPlan p;
                 p.W = q->spec_W;
                 p.C = std::max(128, q->spec_W / 32);   // W + C steps per lane, <= 1/32 redundancy growth
@@ -1562,27 +1609,33 @@ static int iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, i
                 const size_t need = k::spec_scratch_bytes(p.nchunks, q->ncomp(), q->fsz());
                 p.scratch = q->sc1.ensure(need, q->device);
                 k::iir_spec(q->cplx, d, dx, n, q->st32.as<float>(), p, dy, e.stream);
-            } else if (q->mode == LDSP_MODE_EXACT) {
-                q->state_to(false, e.stream);
+                break;
+            }
+            case kSeq:
+                q->state_to(IirObj::kSt32, e.stream);
                 k::iir_seq(q->cplx, d, dx, n, q->st32.as<float>(), dy, e.stream);
-            } else if (q->J1p > 0 && LDSP_KNOB("LDSP_IIR_1P", 0)) {
-                // single pass (tuning builds only: measured 2.75 ms against 0.88 ms for the
-                // blocked scan at 64 Mi): reads st64 (the call's
-                // start), writes st64b (its end); then swap
-                q->state_to(true, e.stream);
-                const k::Iir1pPlan p = q->one_pass_plan(n);
-                k::iir_1p(q->cplx, d, q->b.data(), q->a.data(), dx, n, q->st64.as<double>(), q->st64b.as<double>(), p,
-                          dy, e.stream);
-                std::swap(q->st64.p, q->st64b.p);
-                std::swap(q->st64.cap, q->st64b.cap);
-            } else if (q->D <= k::kIirBlkMaxD && !LDSP_KNOB("LDSP_IIR_OLDSCAN", 0)) {
-                q->state_to(true, e.stream);
+                break;
+            case kModal: {  // one pass: reads mst (the call's start), writes mstb (its end); then swap
+                q->state_to(IirObj::kStModal, e.stream);
+                const k::IirModalPlan p = q->modal_plan(n);
+                k::iir_modal(q->cplx, q->mf.cf, dx, n, q->mst.as<double>(), q->mstb.as<double>(), p, dy, e.stream,
+                             iq16);
+                std::swap(q->mst.p, q->mstb.p);
+                std::swap(q->mst.cap, q->mstb.cap);
+                break;
+            }
+            case kBlk: {
+                q->state_to(IirObj::kSt64, e.stream);
                 const k::IirBlkPlan p = q->blk_plan(n);
                 k::iir_blk(q->cplx, d, q->b.data(), q->a.data(), dx, n, q->st64.as<double>(), p, dy, e.stream, iq16);
-            } else {
-                q->state_to(true, e.stream);
+                break;
+            }
+            case kScan: {
+                q->state_to(IirObj::kSt64, e.stream);
                 const k::IirScanPlan p = q->scan_plan(n);
                 k::iir_scan(q->cplx, d, dx, n, q->st64.as<double>(), p, dy, e.stream);
+                break;
+            }
             }
         }
         q->ord.mark(e.stream);

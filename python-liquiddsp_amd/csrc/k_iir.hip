@@ -20,6 +20,7 @@
 
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
+#include "ldsp_math.hpp"
 
 namespace ldsp {
 namespace k {
@@ -670,17 +671,6 @@ __device__ __forceinline__ void mv_acc(const double* __restrict__ M, const doubl
 // The staging tiles and the scan buffer share LDS (they are used in separate
 // phases, fenced by __syncthreads): 35 KB per block, and at most 168 VGPRs, so
 // three blocks (12 waves) fit a CU to hide the HBM latency of the tile stream.
-// (float)v / 32767.0f for int16 v without the IEEE division sequence: the
-// product with fl(1/32767) corrected by one fma residual step.  Equal to the
-// correctly rounded quotient for all 65 536 inputs
-// (scripts/analysis/check_iq16_div.py, tests/test_oracle_math.py).
-__device__ __forceinline__ float iq16_to_f(short v)
-{
-    constexpr float d = 32767.0f, r = 1.0f / 32767.0f;
-    const float f = (float)v;
-    const float q0 = f * r;
-    return fmaf(fmaf(-q0, d, f), r, q0);
-}
 
 // IQ16: the input is the SDR wire format (int16 I, Q pairs) converted on load
 // exactly as bytes_to_iq (utility.hpp:61-69: (float)v / 32767.0f), so a chain
@@ -862,240 +852,6 @@ k_iir_blk(Step step, const void* __restrict__ xf, long n, long nch, const double
             for (int i = 0; i < D; i++) state64[c * D + i] = v[c][i];
 }
 
-// out += M in with M streamed row by row (M per lane or uniform, in global
-// memory): keeps at most one row of M in registers.
-template <int D>
-__device__ __forceinline__ void mv_rows(const double* __restrict__ M, const double (&in)[D], double (&out)[D])
-{
-#pragma unroll
-    for (int r = 0; r < D; r++) {
-        double m[D];
-#pragma unroll
-        for (int q = 0; q < D; q++) m[q] = M[r * D + q];
-        double acc = out[r];
-#pragma unroll
-        for (int q = 0; q < D; q++) acc = fma(m[q], in[q], acc);
-        out[r] = acc;
-        __builtin_amdgcn_sched_barrier(0);     // one row in flight: no hoisting of the next row's loads
-    }
-}
-
-// --------------------------------------------------------------- single-pass float64 scan
-// k_iir_1p (D <= 8; the default fast path when the filter forgets its state
-// within kIir1pJmax blocks): the input is read once.  Block b (dynamic ticket
-// order) owns kIir1pBlock = kBN x kOC samples, one kOC-sample chunk per thread,
-// staged through LDS tiles into registers.
-//   1. every chunk from a zero state -> L_j; in-block inclusive scan
-//      E_j = L_j + A^{kOC} E_{j-1}; the block's end-from-zero state BL_b = E_255
-//      is published (flag = this call's epoch).
-//   2. the block's true start state needs only the J preceding blocks:
-//      S_b = sum_{i=1..min(b,J)} A^{kOB (i-1)} BL_{b-i}  (+ A^{kOB b} S_call, b < J)
-//      -- older blocks contribute through A^{kOB J}, which the host checked is
-//      below 2^-70 (the same float64 result).  Blocks only wait for blocks with
-//      smaller tickets, which are running or done: no deadlock.
-//   3. chunk j starts from E_{j-1} + A^{kOC j} S_b and re-runs, writing its
-//      outputs through the LDS tiles.
-// HBM traffic: the input once (pass 2 re-reads the block's 64 KiB from L2, where
-// pass 1 has just brought it), the output once: 16 B per complex sample.
-constexpr int kOC = 32;                          // samples per chunk (thread)
-static_assert(kIir1pBlock == kBN * kOC, "kernels.hpp block size");
-
-template <int NC, int D, class Step>
-__global__ void __launch_bounds__(kBN) k_iir_1p(Step step, const float* __restrict__ xf, long n, long nblk,
-                                                Iir1pPlan p, const double* __restrict__ st_in,
-                                                double* __restrict__ st_out, float* __restrict__ yf)
-{
-    using S = SampT<NC>;
-    using T = typename S::T;
-    constexpr int kRow = kBT + 1;
-    constexpr int DD = D * D;
-    constexpr size_t kStage = sizeof(T) * (kBN / 64) * 64 * kRow, kScn = sizeof(double) * kBN * NC * D;
-    __shared__ __attribute__((aligned(16))) char lds[kStage > kScn ? kStage : kScn];
-    __shared__ double lb[kIir1pJmax + 1][NC][D];
-    __shared__ long sh_b;
-    T (*stage)[64 * kRow] = reinterpret_cast<T (*)[64 * kRow]>(lds);
-    double (*scn)[NC][D] = reinterpret_cast<double (*)[NC][D]>(lds);
-    const T* __restrict__ x = (const T*)xf;
-    T* __restrict__ y = (T*)yf;
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wave = t >> 6;
-    if (t == 0) sh_b = (long)atomicAdd(p.ticket, 1u);
-    __syncthreads();
-    const long b = sh_b;
-    if (b == nblk - 1 && t == 0) *p.ticket = 0u;            // every ticket is taken: ready for the next call
-    const long wbase = (b * kBN + wave * 64) * (long)kOC;    // first sample of this wave's 64 chunks
-    const long cbase = (b * kBN + t) * (long)kOC;            // first sample of this lane's chunk
-    const long rem = n - cbase;                              // samples of this chunk inside the call
-    T* st = stage[wave];
-    double v[NC][D];
-    // This lane's chunk over the staged tiles (coalesced loads, transposed
-    // through LDS), from state v; WRITE: outputs back through the tiles.  Pass 2
-    // re-reads the block's 64 KiB of input, which pass 1 has just brought into
-    // L2, so HBM sees it once.
-    auto run = [&](auto write_tag) {
-        constexpr bool WRITE = decltype(write_tag)::value;
-#pragma unroll
-        for (int k = 0; k < kOC / kBT; k++) {
-            T raw[kBT];
-#pragma unroll
-            for (int q = 0; q < kBT; q++) {
-                const int e = lane + 64 * q;
-                const long gi = wbase + (long)(e >> 4) * kOC + k * kBT + (e & 15);
-                T z{};
-                raw[q] = gi < n ? x[gi] : z;
-            }
-#pragma unroll
-            for (int q = 0; q < kBT; q++) {
-                const int e = lane + 64 * q;
-                st[(e >> 4) * kRow + (e & 15)] = raw[q];
-            }
-            iir_wave_sync();
-            T in[kBT];
-#pragma unroll
-            for (int i = 0; i < kBT; i++) in[i] = st[lane * kRow + i];
-            iir_wave_sync();
-#pragma unroll
-            for (int i = 0; i < kBT; i++) {
-                T o{};
-                if (k * kBT + i < rem)
-#pragma unroll
-                    for (int c = 0; c < NC; c++) {
-                        const double r = step(v[c], S::get(in[i], c));
-                        if (WRITE) S::put(o, c, (float)r);
-                    }
-                if (WRITE) st[lane * kRow + i] = o;
-            }
-            if (WRITE) {
-                iir_wave_sync();
-#pragma unroll
-                for (int q = 0; q < kBT; q++) {
-                    const int e = lane + 64 * q;
-                    const long gi = wbase + (long)(e >> 4) * kOC + k * kBT + (e & 15);
-                    if (gi < n) y[gi] = st[(e >> 4) * kRow + (e & 15)];
-                }
-                iir_wave_sync();
-            }
-        }
-    };
-    // 1. from a zero state
-    double E[NC][D];
-#pragma unroll
-    for (int c = 0; c < NC; c++)
-#pragma unroll
-        for (int i = 0; i < D; i++) v[c][i] = 0.0;
-    run(std::false_type{});
-#pragma unroll
-    for (int c = 0; c < NC; c++)
-#pragma unroll
-        for (int i = 0; i < D; i++) E[c][i] = v[c][i];
-    __syncthreads();                     // every wave done with the staging tiles (same LDS)
-#pragma unroll
-    for (int c = 0; c < NC; c++)
-#pragma unroll
-        for (int i = 0; i < D; i++) scn[t][c][i] = E[c][i];
-    __syncthreads();
-#pragma unroll 1
-    for (int l = 0; (1 << l) < kBN; l++) {
-        const int dd = 1 << l;
-        if (t >= dd) {
-#pragma unroll
-            for (int c = 0; c < NC; c++) {
-                double o[D];
-#pragma unroll
-                for (int i = 0; i < D; i++) o[i] = scn[t - dd][c][i];
-                mv_rows<D>(p.AC + (size_t)dd * DD, o, E[c]);
-            }
-        }
-        __syncthreads();
-        if (t >= dd)
-#pragma unroll
-            for (int c = 0; c < NC; c++)
-#pragma unroll
-                for (int i = 0; i < D; i++) scn[t][c][i] = E[c][i];
-        __syncthreads();
-    }
-    if (t == kBN - 1) {                  // publish BL_b
-#pragma unroll
-        for (int c = 0; c < NC; c++)
-#pragma unroll
-            for (int i = 0; i < D; i++) p.agg[(b * NC + c) * D + i] = E[c][i];
-        __threadfence();
-        __hip_atomic_store(p.flags + b, p.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // 2. look-back: thread i (< J) adds A^{kOB i} BL_{b-1-i}; where b-1-i = -1, the call's start state
-    double tm[NC][D];
-#pragma unroll
-    for (int c = 0; c < NC; c++)
-#pragma unroll
-        for (int i = 0; i < D; i++) tm[c][i] = 0.0;
-    if (t < p.J && t <= b) {
-        const long bb = b - 1 - t;
-        const double* src = st_in;
-        if (bb >= 0) {
-            unsigned spins = 0;
-            while (__hip_atomic_load(p.flags + bb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != p.epoch) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24)) break;   // bounded wait: a lost flag cannot hang the device
-            }
-            src = p.agg + bb * NC * D;
-        }
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            double in[D];
-#pragma unroll
-            for (int i = 0; i < D; i++) in[i] = __hip_atomic_load(src + c * D + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            mv_rows<D>(p.AB + (size_t)t * DD, in, tm[c]);
-        }
-    }
-    if (t < kIir1pJmax)
-#pragma unroll
-        for (int c = 0; c < NC; c++)
-#pragma unroll
-            for (int i = 0; i < D; i++) lb[t][c][i] = tm[c][i];
-    __syncthreads();
-    if (t < NC * D) {                    // element t of S_b: the look-back terms summed in a fixed order
-        double a = 0.0;
-        for (int q = 0; q < kIir1pJmax; q++) a += (&lb[q][0][0])[t];
-        (&lb[kIir1pJmax][0][0])[t] = a;
-    }
-    __syncthreads();
-    double Sb[NC][D];
-#pragma unroll
-    for (int c = 0; c < NC; c++)
-#pragma unroll
-        for (int i = 0; i < D; i++) Sb[c][i] = lb[kIir1pJmax][c][i];
-    // 3. chunk t's true start state: E_{t-1} + A^{kOC t} S_b
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-        if (t == 0) {
-#pragma unroll
-            for (int i = 0; i < D; i++) v[c][i] = Sb[c][i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < D; i++) v[c][i] = scn[t - 1][c][i];
-            mv_rows<D>(p.AC + (size_t)t * DD, Sb[c], v[c]);
-        }
-    }
-    __syncthreads();                     // scan buffer read: the staging tiles reuse it
-    run(std::true_type{});
-    if (rem > 0 && rem <= kOC)           // the chunk holding sample n - 1: the call's end state
-#pragma unroll
-        for (int c = 0; c < NC; c++)
-#pragma unroll
-            for (int i = 0; i < D; i++) st_out[c * D + i] = v[c][i];
-}
-
-template <int NC, int D, class Step>
-void launch_1p(const Step& st, const float* x, size_t n, const Iir1pPlan& p, const double* st_in, double* st_out,
-               float* y, hipStream_t s)
-{
-    const long nblk = (long)((n + kIir1pBlock - 1) / kIir1pBlock);
-    LDSP_PROF(s, "k_iir_1p");
-    hipLaunchKernelGGL((k_iir_1p<NC, D, Step>), dim3((unsigned)nblk), dim3(kBN), 0, s, st, x, (long)n, nblk, p, st_in,
-                       st_out, y);
-}
-
 template <int NC, int D, class Step, bool IQ16 = false>
 void launch_blk(const Step& st, const IirDesc& d, const void* x, size_t n, double* state64, const IirBlkPlan& p,
                 float* y, hipStream_t s)
@@ -1149,30 +905,6 @@ void dispatch_blk(const IirDesc& d, const float* cb, const float* ca, const void
             st.a[i] = i < d.na ? (double)ca[i] : 0.0;
         }
         launch_blk<NC, D, StepTf<D>, IQ16>(st, d, x, n, state64, p, y, s);
-    }
-}
-
-template <int NC, int D>
-void dispatch_1p(const IirDesc& d, const float* cb, const float* ca, const float* x, size_t n, const double* st_in,
-                 double* st_out, const Iir1pPlan& p, float* y, hipStream_t s)
-{
-    if (d.sos) {
-        if constexpr (D % 2 == 0) {
-            StepSos<D> st;
-            for (int q = 0; q < D / 2; q++)
-                for (int k = 0; k < 3; k++) {
-                    st.b[q][k] = (double)cb[3 * q + k];
-                    st.a[q][k] = (double)ca[3 * q + k];
-                }
-            launch_1p<NC, D>(st, x, n, p, st_in, st_out, y, s);
-        }
-    } else {
-        StepTf<D> st;
-        for (int i = 0; i <= D; i++) {
-            st.b[i] = i < d.nb ? (double)cb[i] : 0.0;
-            st.a[i] = i < d.na ? (double)ca[i] : 0.0;
-        }
-        launch_1p<NC, D>(st, x, n, p, st_in, st_out, y, s);
     }
 }
 
@@ -1306,25 +1038,5 @@ void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, cons
 #undef LDSP_BLK
 }
 
-void iir_1p(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n,
-            const double* st_in, double* st_out, const Iir1pPlan& p, void* y, hipStream_t s)
-{
-    if (n == 0) return;
-    LDSP_REQUIRE(d.D >= 1 && d.D <= kIirBlkMaxD, "iir: state dimension too large for the single-pass scan");
-    LDSP_REQUIRE(p.J >= 1 && p.J <= kIir1pJmax, "iir: look-back depth out of range");
-    const float* xf = (const float*)x;
-    float* yf = (float*)y;
-#define LDSP_1P(DD)                                                                           \
-    case DD:                                                                                  \
-        if (cplx) dispatch_1p<2, DD>(d, hb, ha, xf, n, st_in, st_out, p, yf, s);               \
-        else dispatch_1p<1, DD>(d, hb, ha, xf, n, st_in, st_out, p, yf, s);                    \
-        break;
-    switch (d.D) {
-        LDSP_1P(1) LDSP_1P(2) LDSP_1P(3) LDSP_1P(4) LDSP_1P(5) LDSP_1P(6) LDSP_1P(7) LDSP_1P(8)
-    default: throw Error(LDSP_EUNSUP, "iir: unsupported state dimension");
-    }
-#undef LDSP_1P
-    LDSP_HIP(hipGetLastError());
-}
 } // namespace k
 } // namespace ldsp

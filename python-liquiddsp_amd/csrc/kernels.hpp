@@ -112,23 +112,36 @@ struct IirBlkPlan {
 // iq16: x holds int16 (I, Q) pairs, converted on load as bytes_to_iq does
 void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n, double* state64,
              const IirBlkPlan& p, void* y, hipStream_t s, bool iq16 = false);
-// Single-pass float64 scan (k_iir_1p, D <= 8): blocks of kIir1pBlock samples
-// (32 per thread), each block's start state from the J <= kIir1pJmax blocks
-// before it (decoupled look-back; valid when ||A^(kIir1pBlock J)|| < 2^-70).
-constexpr int kIir1pBlock = 8192;
-constexpr int kIir1pJmax = 8;
-struct Iir1pPlan {
-    int J;                // look-back depth (blocks)
-    const double* AC;     // A^{32 j}, j = 0..255                       [256][D*D]
-    const double* AB;     // A^{kIir1pBlock j}, j = 0..J-1              [J][D*D]
-    double* agg;          // [nblk][ncomp][D] each block's end state from a zero start
-    unsigned* flags;      // [nblk] = epoch once agg[b] is published (zeroed when allocated)
-    unsigned* ticket;     // dynamic block order (zero between calls)
-    unsigned epoch;       // per call, never 0
+// Single-pass float64 scan in modal coordinates (k_iir_modal.hip): the filter
+// as M <= 8 first-order complex modes, z_k <- lambda_k z_k + u, y = d u +
+// sum_k Re(g_k z_k) (pair weights folded into g).  One wave = 64 chunks of
+// kIirModalChunk samples; each wave's start state is the look-back sum over the
+// J <= kIirModalJmax waves before it (valid when max|lambda|^(2048 J) < 2^-70).
+// State layout (st_in / st_out, distinct buffers): double [ncomp][M][re, im].
+constexpr int kIirModalMax = 8;
+constexpr int kIirModalChunk = 32;
+constexpr int kIirModalJmax = 64;
+struct IirModalCoef {     // kernel argument
+    int M;
+    double lr[kIirModalMax], li[kIirModalMax];   // lambda_k
+    double gr[kIirModalMax], gi[kIirModalMax];   // g_k (x2 for a conjugate pair)
+    double l2r[kIirModalMax], l2i[kIirModalMax];  // lambda_k^2
+    double d;                                    // direct term
 };
-// st_in: the call's start state, st_out: its end state (distinct buffers)
-void iir_1p(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n,
-            const double* st_in, double* st_out, const Iir1pPlan& p, void* y, hipStream_t s);
+struct IirModalPlan {
+    int J;                // look-back depth (waves)
+    const double* PS;     // [6][M][re, im]   lambda^(32 * 2^l), l = 0..5
+    const double* PL;     // [64][M][re, im]  lambda^(32 t), t = lane
+    const double* PB;     // [J][M][re, im]   lambda^(2048 i)
+    uint64_t* agg;        // [nunits][ncomp][M * 4] {32-bit half, epoch} granules (zeroed when allocated)
+    uint32_t epoch;       // per call, never 0
+    int recompute = 0;    // test hook: every wave recomputes its predecessors instead of reading them
+    int variant = 0;      // tuning builds only (timing experiments, wrong outputs): bit 0 no look-back,
+                          // bit 1 no pass 2, bit 2 no pass 1 / scan
+};
+long iir_modal_units(size_t n);   // workgroups (2048-sample look-back units) of a call
+void iir_modal(bool cplx, const IirModalCoef& cf, const void* x, size_t n, const double* st_in, double* st_out,
+               const IirModalPlan& p, void* y, hipStream_t s, bool iq16 = false);
 // Speculative exact evaluation for fast-decaying filters: chunks start from a
 // zero state W samples early; a verifier re-runs any chunk whose guessed
 // start state differs bit-wise from its predecessor's end state.

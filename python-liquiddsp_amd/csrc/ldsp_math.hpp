@@ -26,6 +26,18 @@ __host__ __device__ inline float bitsf(uint32_t u) { return __builtin_bit_cast(f
 __host__ __device__ inline float fabs_(float x) { return bitsf(fbits(x) & 0x7fffffffu); }
 __host__ __device__ inline float sel(bool c, float a, float b) { return c ? a : b; }
 
+// (float)v / 32767.0f for int16 v (bytes_to_iq, reference src/utility.hpp:61-69)
+// without the IEEE division sequence: the product with fl(1/32767) corrected by
+// one fma residual step.  Equal to the correctly rounded quotient for all 65 536
+// inputs (scripts/analysis/check_iq16_div.py, tests/test_oracle_math.py).
+__device__ __forceinline__ float iq16_to_f(short v)
+{
+    constexpr float d = 32767.0f, r = 1.0f / 32767.0f;
+    const float f = (float)v;
+    const float q0 = f * r;
+    return fmaf(fmaf(-q0, d, f), r, q0);
+}
+
 // e^x (fdlibm e_expf.c): x = k ln2 + r, rational kernel for e^r
 __host__ __device__ inline float lm_expf(float x)
 {

@@ -1,0 +1,370 @@
+// modal.cpp -- host construction and check of an IIR filter's modal form
+// (modal.hpp), in long double.
+//
+// For the recursion s' = A s + B u, y = C s + Dd u with D distinct poles
+// lambda_k (eigenvalues of A): eigenvectors w_k by inverse iteration, beta =
+// W^-1 B, V = W diag(beta) (so V^-1 B = 1), g = C V.  With z = V^-1 s:
+//     z_k' = lambda_k z_k + u,    y = Dd u + sum_k g_k z_k.
+// For a real filter the non-real poles come in conjugate pairs whose modes are
+// conjugate for real input: one mode per pair carries weight 2 (y gets
+// 2 Re(g_k z_k)), a real pole one mode of weight 1.  The form is accepted only
+// when it reproduces the long-double state-space recursion to 1e-10 (impulse +
+// noise input, the free response of a random state, and the state round trip);
+// clustered poles (narrow high-order Butterworth / Chebyshev-I designs) make V
+// ill-conditioned and fail here, keeping the SOS-coordinate scan.
+#include "modal.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace ldsp {
+
+namespace {
+
+using ld = long double;
+using cld = std::complex<long double>;
+
+// A (n x n) X = B (n x m) by Gaussian elimination with partial pivoting; false if singular
+bool csolve(std::vector<cld> A, std::vector<cld>& X, int n, int m)
+{
+    for (int col = 0; col < n; col++) {
+        int piv = col;
+        ld best = std::abs(A[col * n + col]);
+        for (int r = col + 1; r < n; r++) {
+            const ld v = std::abs(A[r * n + col]);
+            if (v > best) {
+                best = v;
+                piv = r;
+            }
+        }
+        if (!(best > 0)) return false;
+        if (piv != col) {
+            for (int c = 0; c < n; c++) std::swap(A[col * n + c], A[piv * n + c]);
+            for (int c = 0; c < m; c++) std::swap(X[col * m + c], X[piv * m + c]);
+        }
+        for (int r = col + 1; r < n; r++) {
+            const cld f = A[r * n + col] / A[col * n + col];
+            if (f == cld(0)) continue;
+            for (int c = col; c < n; c++) A[r * n + c] -= f * A[col * n + c];
+            for (int c = 0; c < m; c++) X[r * m + c] -= f * X[col * m + c];
+        }
+    }
+    for (int row = n - 1; row >= 0; row--)
+        for (int c = 0; c < m; c++) {
+            cld s = X[row * m + c];
+            for (int k = row + 1; k < n; k++) s -= A[row * n + k] * X[k * m + c];
+            X[row * m + c] = s / A[row * n + row];
+        }
+    return true;
+}
+
+cld cpow_u(cld z, unsigned long long e)
+{
+    cld r(1);
+    while (e) {
+        if (e & 1) r *= z;
+        z *= z;
+        e >>= 1;
+    }
+    return r;
+}
+
+// deterministic input for the host check: uniform in [-1, 1)
+struct Lcg {
+    uint64_t s = 0x9e3779b97f4a7c15ull;
+    double next()
+    {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        return (double)(s >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+    }
+};
+
+} // namespace
+
+std::vector<cld> sos_poles(const std::vector<float>& a, unsigned nsos)
+{
+    std::vector<cld> p;
+    for (unsigned s = 0; s < nsos; s++) {
+        const ld a1 = a[3 * s + 1], a2 = a[3 * s + 2];
+        const ld disc = a1 * a1 - 4 * a2;
+        if (disc >= 0) {   // q = -(a1 + sign(a1) sqrt(disc)) / 2: roots q and a2 / q
+            const ld r = std::sqrt(disc);
+            const ld q = -0.5L * (a1 + (a1 >= 0 ? r : -r));
+            p.push_back(cld(q, 0));
+            p.push_back(cld(q != 0 ? a2 / q : 0, 0));
+        } else {
+            const ld im = std::sqrt(-disc) / 2;
+            p.push_back(cld(-a1 / 2, im));
+            p.push_back(cld(-a1 / 2, -im));
+        }
+    }
+    return p;
+}
+
+std::vector<cld> tf_poles(const std::vector<float>& a, int na, int D)
+{
+    // Durand-Kerner on z^D + c1 z^(D-1) + ... + cD, then Newton polishing
+    std::vector<ld> c(D + 1, 0);
+    c[0] = 1;
+    for (int i = 1; i <= D; i++) c[i] = i < na ? (ld)a[i] : 0;
+    auto P = [&](cld z) {
+        cld v(1);
+        for (int i = 1; i <= D; i++) v = v * z + c[i];
+        return v;
+    };
+    auto dP = [&](cld z) {
+        cld v(0), d(0);
+        cld p(1);
+        for (int i = 1; i <= D; i++) {
+            d = d * z + p;
+            p = p * z + c[i];
+        }
+        (void)v;
+        return d;
+    };
+    ld R = 1;
+    for (int i = 1; i <= D; i++) R = std::max(R, 1 + std::abs(c[i]));
+    std::vector<cld> z(D);
+    const cld seed(0.4L, 0.9L);
+    for (int k = 0; k < D; k++) z[k] = R * cpow_u(seed, k + 1) / std::abs(cpow_u(seed, k + 1));
+    for (int it = 0; it < 2000; it++) {
+        ld moved = 0;
+        for (int k = 0; k < D; k++) {
+            cld den(1);
+            for (int j = 0; j < D; j++)
+                if (j != k) den *= z[k] - z[j];
+            if (den == cld(0)) continue;
+            const cld dz = P(z[k]) / den;
+            z[k] -= dz;
+            moved = std::max(moved, std::abs(dz));
+        }
+        if (moved < 1e-19L) break;
+    }
+    for (int k = 0; k < D; k++)
+        for (int it = 0; it < 4; it++) {
+            const cld d = dP(z[k]);
+            if (d == cld(0)) break;
+            z[k] -= P(z[k]) / d;
+        }
+    return z;
+}
+
+ModalForm modal_form(int D, const std::vector<ld>& A, const std::vector<ld>& B, const std::vector<ld>& C, ld Dd,
+                     const std::vector<cld>& poles)
+{
+    ModalForm f;
+    f.D = D;
+    auto fail = [&](const char* why) {
+        f.ok = false;
+        f.why = why;
+        return f;
+    };
+    if (D < 1 || D > 2 * k::kIirModalMax || (int)poles.size() != D) return fail("state dimension");
+    ld lmax = 0, anorm = 0;
+    for (int i = 0; i < D; i++) {
+        lmax = std::max(lmax, std::abs(poles[i]));
+        for (int j = i + 1; j < D; j++)
+            if (std::abs(poles[i] - poles[j]) <= 1e-9L * std::max<ld>(1, std::abs(poles[i])))
+                return fail("repeated pole");
+        ld row = 0;
+        for (int j = 0; j < D; j++) row += std::fabs(A[i * D + j]);
+        anorm = std::max(anorm, row);
+    }
+    if (!(lmax < 1)) return fail("pole on or outside the unit circle");
+
+    // eigenvectors (columns of W) by inverse iteration with a slightly shifted pole
+    std::vector<cld> W(D * D);
+    for (int k = 0; k < D; k++) {
+        const ld sc = 1 + std::abs(poles[k]);
+        const cld mu = poles[k] + cld(1e-12L * sc, 0.7e-12L * sc);
+        std::vector<cld> x(D);
+        for (int i = 0; i < D; i++) x[i] = cld(1 + 0.1L * i, 0.05L * i);
+        for (int it = 0; it < 4; it++) {
+            std::vector<cld> Mx(D * D);
+            for (int i = 0; i < D; i++)
+                for (int j = 0; j < D; j++) Mx[i * D + j] = cld(A[i * D + j]) - (i == j ? mu : cld(0));
+            if (!csolve(Mx, x, D, 1)) return fail("eigenvector");
+            ld nrm = 0;
+            for (int i = 0; i < D; i++) nrm += std::norm(x[i]);
+            nrm = std::sqrt(nrm);
+            if (!(nrm > 0) || !std::isfinite((double)nrm)) return fail("eigenvector");
+            for (int i = 0; i < D; i++) x[i] /= nrm;
+        }
+        ld res = 0;
+        for (int i = 0; i < D; i++) {
+            cld r = -poles[k] * x[i];
+            for (int j = 0; j < D; j++) r += A[i * D + j] * x[j];
+            res = std::max(res, std::abs(r));
+        }
+        if (res > 1e-10L * (1 + anorm)) return fail("eigenvector residual");
+        for (int i = 0; i < D; i++) W[i * D + k] = x[i];
+    }
+    std::vector<cld> beta(D);
+    for (int i = 0; i < D; i++) beta[i] = cld(B[i]);
+    if (!csolve(W, beta, D, 1)) return fail("eigenvectors dependent");
+    std::vector<cld> V(D * D), g(D, cld(0));
+    for (int k = 0; k < D; k++) {
+        if (!(std::abs(beta[k]) > 0)) return fail("mode not driven by the input");
+        for (int i = 0; i < D; i++) {
+            V[i * D + k] = W[i * D + k] * beta[k];
+            g[k] += C[i] * V[i * D + k];
+        }
+    }
+    std::vector<cld> Vi(D * D, cld(0));
+    for (int i = 0; i < D; i++) Vi[i * D + i] = 1;
+    if (!csolve(V, Vi, D, D)) return fail("modal basis singular");
+
+    // one mode per conjugate pair (weight 2) or real pole (weight 1)
+    std::vector<int> rep;
+    std::vector<int> wt;
+    int npair = 0, nreal = 0, nneg = 0;
+    for (int k = 0; k < D; k++) {
+        const ld im = poles[k].imag(), tol = 1e-12L * std::max<ld>(1, std::abs(poles[k]));
+        if (std::fabs(im) <= tol) {
+            rep.push_back(k);
+            wt.push_back(1);
+            nreal++;
+        } else if (im > 0) {
+            bool partner = false;
+            for (int j = 0; j < D; j++)
+                if (poles[j].imag() < 0 &&
+                    std::abs(poles[j] - std::conj(poles[k])) <= 1e-9L * std::max<ld>(1, std::abs(poles[k])))
+                    partner = true;
+            if (!partner) return fail("complex pole without its conjugate");
+            rep.push_back(k);
+            wt.push_back(2);
+            npair++;
+        } else {
+            nneg++;
+        }
+    }
+    if (nneg != npair || 2 * npair + nreal != D) return fail("pole pairing");
+    const int M = (int)rep.size();
+    if (M > k::kIirModalMax) return fail("too many modes");
+    f.M = M;
+
+    f.cf = k::IirModalCoef{};
+    f.cf.M = M;
+    f.cf.d = (double)Dd;
+    std::vector<cld> lam(M), gw(M);
+    for (int m = 0; m < M; m++) {
+        const int k = rep[m];
+        const bool real = wt[m] == 1;
+        lam[m] = real ? cld(poles[k].real(), 0) : poles[k];
+        gw[m] = (ld)wt[m] * (real ? cld(g[k].real(), 0) : g[k]);
+        const cld l2 = lam[m] * lam[m];
+        f.cf.lr[m] = (double)lam[m].real();
+        f.cf.li[m] = (double)lam[m].imag();
+        f.cf.gr[m] = (double)gw[m].real();
+        f.cf.gi[m] = (double)gw[m].imag();
+        f.cf.l2r[m] = (double)l2.real();
+        f.cf.l2i[m] = (double)l2.imag();
+    }
+    f.to_s.assign((size_t)D * M, 0);
+    f.to_z.assign((size_t)M * D, 0);
+    for (int m = 0; m < M; m++) {
+        const int k = rep[m];
+        const bool real = wt[m] == 1;
+        for (int i = 0; i < D; i++) {
+            const cld v = (ld)wt[m] * V[i * D + k];
+            f.to_s[(size_t)i * M + m] = std::complex<double>((double)v.real(), real ? 0.0 : (double)v.imag());
+            const cld r = Vi[k * D + i];
+            f.to_z[(size_t)m * D + i] = std::complex<double>((double)r.real(), real ? 0.0 : (double)r.imag());
+        }
+    }
+
+    // host check: the double-precision modal recursion (the kernel's formulas)
+    // against the long-double state-space recursion
+    auto modal_step = [&](std::vector<std::complex<double>>& z, double u) {
+        double y = f.cf.d * u;
+        for (int m = 0; m < M; m++) {
+            y = std::fma(f.cf.gr[m], z[m].real(), y);
+            y = std::fma(-f.cf.gi[m], z[m].imag(), y);
+            const double nr = std::fma(f.cf.lr[m], z[m].real(), std::fma(-f.cf.li[m], z[m].imag(), u));
+            const double ni = std::fma(f.cf.li[m], z[m].real(), f.cf.lr[m] * z[m].imag());
+            z[m] = std::complex<double>(nr, ni);
+        }
+        return y;
+    };
+    auto ss_step = [&](std::vector<ld>& s, ld u) {
+        ld y = Dd * u;
+        for (int i = 0; i < D; i++) y += C[i] * s[i];
+        std::vector<ld> t(D, 0);
+        for (int i = 0; i < D; i++) {
+            ld v = B[i] * u;
+            for (int j = 0; j < D; j++) v += A[i * D + j] * s[j];
+            t[i] = v;
+        }
+        s = t;
+        return y;
+    };
+    Lcg rng;
+    double err = 0;
+    {   // impulse + noise from rest
+        std::vector<std::complex<double>> z(M, 0.0);
+        std::vector<ld> s(D, 0);
+        double ymax = 0, dmax = 0;
+        for (int n = 0; n < 4096; n++) {
+            const double u = n == 0 ? 1.0 : rng.next();
+            const ld ys = ss_step(s, u);
+            const double ym = modal_step(z, u);
+            ymax = std::max(ymax, (double)std::fabs(ys));
+            dmax = std::max(dmax, std::fabs(ym - (double)ys));
+        }
+        err = std::max(err, ymax > 0 ? dmax / ymax : dmax);
+    }
+    {   // a random state: round trip and free response
+        std::vector<ld> s(D);
+        double smax = 0;
+        for (int i = 0; i < D; i++) {
+            s[i] = rng.next();
+            smax = std::max(smax, (double)std::fabs(s[i]));
+        }
+        std::vector<std::complex<double>> z(M, 0.0);
+        for (int m = 0; m < M; m++)
+            for (int i = 0; i < D; i++) z[m] += f.to_z[(size_t)m * D + i] * (double)s[i];
+        double dmax = 0;
+        for (int i = 0; i < D; i++) {
+            double v = 0;
+            for (int m = 0; m < M; m++) v += (f.to_s[(size_t)i * M + m] * z[m]).real();
+            dmax = std::max(dmax, std::fabs(v - (double)s[i]));
+        }
+        err = std::max(err, dmax / smax);
+        double ymax = 0;
+        dmax = 0;
+        for (int n = 0; n < 512; n++) {
+            const ld ys = ss_step(s, 0);
+            const double ym = modal_step(z, 0.0);
+            ymax = std::max(ymax, (double)std::fabs(ys));
+            dmax = std::max(dmax, std::fabs(ym - (double)ys));
+        }
+        if (ymax > 0) err = std::max(err, dmax / ymax);
+    }
+    f.err = err;
+    if (!(err <= 1e-10)) return fail("modal form ill-conditioned");
+
+    // look-back depth: max |lambda|^(2048 J) < 2^-70
+    int J = 1;
+    if (lmax > 0) {
+        const ld need = 70 * std::log(2.0L) / (-(ld)k::kIirModalChunk * 64 * std::log(lmax));
+        J = std::max(1, (int)std::ceil(need));
+    }
+    if (J > k::kIirModalJmax) return fail("decays too slowly for the look-back");
+    f.J = J;
+
+    f.tables.clear();
+    auto put = [&](cld v) {
+        f.tables.push_back((double)v.real());
+        f.tables.push_back((double)v.imag());
+    };
+    for (int l = 0; l < 6; l++)
+        for (int m = 0; m < M; m++) put(cpow_u(lam[m], (unsigned long long)k::kIirModalChunk << l));
+    for (int t = 0; t < 64; t++)
+        for (int m = 0; m < M; m++) put(cpow_u(lam[m], (unsigned long long)k::kIirModalChunk * t));
+    for (int i = 0; i < J; i++)
+        for (int m = 0; m < M; m++) put(cpow_u(lam[m], (unsigned long long)k::kIirModalChunk * 64 * i));
+    f.ok = true;
+    return f;
+}
+
+} // namespace ldsp

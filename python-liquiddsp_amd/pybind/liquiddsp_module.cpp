@@ -355,11 +355,17 @@ struct IIR {
         if (is_device_tensor(b)) {
             py::object& torch = torch_mod();
             py::object t = py::reinterpret_borrow<py::object>(b).attr("reshape")(-1).attr("contiguous")();
+            py::object dt = t.attr("dtype");
+            if (!(dt.equal(torch.attr("int16")) || dt.equal(torch.attr("uint8")) || dt.equal(torch.attr("int8"))))
+                throw py::value_error("from_bytes: the tensor must hold raw bytes or int16 samples (int16 / uint8 / int8)");
             py::object dev = t.attr("device");
             const int tdev = dev.attr("index").cast<int>();
             if (tdev != torch.attr("cuda").attr("current_device")().cast<int>())
                 throw py::value_error("input tensor is not on the current device");
-            const size_t n = t.attr("numel")().cast<size_t>() * t.attr("element_size")().cast<size_t>() / 4;
+            const size_t nbytes = t.attr("numel")().cast<size_t>() * t.attr("element_size")().cast<size_t>();
+            if (nbytes % 4) throw py::value_error("from_bytes: the input must hold whole (I, Q) int16 pairs (a multiple of 4 bytes)");
+            if (reinterpret_cast<uintptr_t>(tptr(t)) % 4) t = t.attr("clone")();   // a view at an odd offset: the kernels read 4-byte pairs
+            const size_t n = nbytes / 4;
             void* s = reinterpret_cast<void*>(
                 torch.attr("cuda").attr("current_stream")(dev).attr("cuda_stream").cast<uintptr_t>());
             py::object out = dev_empty(n, true, dev);
@@ -369,7 +375,9 @@ struct IIR {
         py::object o = py::reinterpret_borrow<py::object>(b);
         if (py::isinstance<py::array>(o)) o = py::module_::import("numpy").attr("ascontiguousarray")(o);
         py::buffer_info bi = py::reinterpret_borrow<py::buffer>(o).request();
-        const size_t n = (size_t)bi.size * (size_t)bi.itemsize / 4;
+        const size_t nbytes = (size_t)bi.size * (size_t)bi.itemsize;
+        if (nbytes % 4) throw py::value_error("from_bytes: the input must hold whole (I, Q) int16 pairs (a multiple of 4 bytes)");
+        const size_t n = nbytes / 4;
         py::array_t<cf> out(n);
         void* yp = out.mutable_data();
         int rc;
@@ -895,7 +903,15 @@ void bind_iir_common(P& c)
         .def("from_bytes", &C::from_bytes, py::arg("byts"),
              "self(bytes_to_iq(byts)) in one pass: int16 (I, Q) pairs converted on load (complex filters)")
         .def_property("exact", &C::get_exact, &C::set_exact)
-        .def("sos", &C::sos);
+        .def("sos", &C::sos)
+        .def("_scan_path", [](C& c, int path) { check(ldsp_debug_iir_path(c.q, path)); },
+             "test hook: 0 automatic, 1 blocked scan, 2 modal scan")
+        .def("_modal_info", [](C& c) {
+            int ok = 0, m = 0, j = 0;
+            double err = 0;
+            check(ldsp_debug_iir_modal_info(c.q, &ok, &m, &j, &err));
+            return py::make_tuple(ok != 0, m, j, err);
+        });
 }
 
 template <typename C>
@@ -935,7 +951,15 @@ void bind_proto(py::module_& m, const char* name)
         .def("print", &C::print)
         .def("reset", &C::reset)
         .def_property("exact", &C::get_exact, &C::set_exact)
-        .def("sos", &C::sos);
+        .def("sos", &C::sos)
+        .def("_scan_path", [](C& c, int path) { check(ldsp_debug_iir_path(c.q, path)); },
+             "test hook: 0 automatic, 1 blocked scan, 2 modal scan")
+        .def("_modal_info", [](C& c) {
+            int ok = 0, m = 0, j = 0;
+            double err = 0;
+            check(ldsp_debug_iir_modal_info(c.q, &ok, &m, &j, &err));
+            return py::make_tuple(ok != 0, m, j, err);
+        });
 }
 
 const char* kResampDoc = "Arbitrary-rate polyphase resampler (liquid resamp_*), runs on the GPU.";

@@ -3,7 +3,7 @@
 `ComplexIIRFilter.from_bytes(raw)` (C ABI `ldsp_iirfilt_execute_iq16`) is
 `filter(bytes_to_iq(raw))` in one pass: reference src/utility.hpp:61-69
 ((float)int16 / 32767.0f per component) followed by iirfilter.hpp:292-298.
-The blocked float64 scan converts on load; the checks:
+The fast scans (modal single pass, blocked) convert on load; the checks:
   * the same bits as the two-call GPU path (bytes_to_iq, then the filter), over
     ragged calls that cut the stream mid-chunk, host and device inputs, and at
     64 Mi samples in one call (the bench size);
@@ -36,11 +36,14 @@ def raw_iq(rng, n):
     return r
 
 
+@pytest.mark.parametrize("path", [2, 1])       # the modal single-pass scan, the blocked scan
 @pytest.mark.parametrize("cuts", [[0, 1, 257, 70_000, 70_001, 1_000_000, 1_048_583], [0, 1_048_583]])
-def test_from_bytes_equals_two_calls(ld, rng, cuts):
+def test_from_bytes_equals_two_calls(ld, rng, cuts, path):
     raw = raw_iq(rng, cuts[-1])
     a = ld.ComplexIIRFilter(**CHAIN_IIR)
     b = ld.ComplexIIRFilter(**CHAIN_IIR)
+    a._scan_path(path)
+    b._scan_path(path)
     for lo, hi in zip(cuts, cuts[1:]):
         seg = raw[2 * lo:2 * hi]
         ya = a.from_bytes(seg.tobytes() if hi - lo < 1000 else seg)

@@ -102,3 +102,22 @@ def test_amradio_readme_blocks_rotating_streams(ld, ora):
     ref = ora.AMRadio()
     refs = [ref(x[i * blk:(i + 1) * blk]) for i in range(nblk)]
     assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), np.concatenate(refs))
+
+
+def test_agc_small_calls_low_bandwidth(ld, ora, rng):
+    """At bandwidth 1e-3 the chunk-parallel threshold grows to ~62 k samples, so
+    calls up to that length run tsa mode: every chunk approximates from the true
+    state over up to ~60 k samples.  Calls at the top of that range stay
+    bit-identical (a trajectory that leaves the exact one is re-run)."""
+    x = _am(rng, 200_000, 48000.0, 300.0)
+    g = ld.AGC()
+    g.bandwidth = 1e-3
+    g.lock = False
+    g.scale = 0.01
+    o = ora.AGC()
+    o.bandwidth = np.float32(1e-3)
+    o.scale = np.float32(0.01)
+    cuts = [0, 10_000, 70_000, 130_000, 190_000, 200_000]
+    ys = [g(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    rs = [o(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    assert_bitwise(np.concatenate(ys), np.concatenate(rs))
