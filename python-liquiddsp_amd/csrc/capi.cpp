@@ -494,15 +494,13 @@ struct IirObj {
             LDSP_HIP(hipMemcpy(d.data(), st64.p, d.size() * 8, hipMemcpyDeviceToHost));
         } else {
             const int M = mf.M;
-            std::vector<double> z(2 * 2 * M);
-            LDSP_HIP(hipMemcpy(z.data(), mst.p, z.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<double> v(2 * 2 * M);
+            LDSP_HIP(hipMemcpy(v.data(), mst.p, v.size() * 8, hipMemcpyDeviceToHost));
             for (int c = 0; c < nc; c++)
                 for (int i = 0; i < D; i++) {
-                    double v = 0;
-                    for (int m = 0; m < M; m++)
-                        v += (mf.to_s[(size_t)i * M + m] *
-                              std::complex<double>(z[(c * M + m) * 2], z[(c * M + m) * 2 + 1])).real();
-                    d[c * D + i] = v;
+                    double t = 0;
+                    for (int q = 0; q < 2 * M; q++) t += mf.from_v[(size_t)i * 2 * M + q] * v[c * 2 * M + q];
+                    d[c * D + i] = t;
                 }
         }
         // 2. float64 layout -> target
@@ -523,15 +521,14 @@ struct IirObj {
             LDSP_HIP(hipMemcpy(st64.p, d.data(), d.size() * 8, hipMemcpyHostToDevice));
         } else {
             const int M = mf.M;
-            std::vector<double> z(2 * 2 * M, 0.0);
+            std::vector<double> v(2 * 2 * M, 0.0);
             for (int c = 0; c < nc; c++)
-                for (int m = 0; m < M; m++) {
-                    std::complex<double> v = 0;
-                    for (int i = 0; i < D; i++) v += mf.to_z[(size_t)m * D + i] * d[c * D + i];
-                    z[(c * M + m) * 2] = v.real();
-                    z[(c * M + m) * 2 + 1] = v.imag();
+                for (int q = 0; q < 2 * M; q++) {
+                    double t = 0;
+                    for (int i = 0; i < D; i++) t += mf.to_v[(size_t)q * D + i] * d[c * D + i];
+                    v[c * 2 * M + q] = t;
                 }
-            LDSP_HIP(hipMemcpy(mst.p, z.data(), z.size() * 8, hipMemcpyHostToDevice));
+            LDSP_HIP(hipMemcpy(mst.p, v.data(), v.size() * 8, hipMemcpyHostToDevice));
         }
         state_at = to;
     }
@@ -590,8 +587,8 @@ struct IirObj {
         k::IirModalPlan p;
         p.J = mf.J;
         p.PS = mtab.as<double>();
-        p.PL = p.PS + 6 * mf.M * 2;
-        p.PB = p.PL + 64 * mf.M * 2;
+        p.PL = p.PS + 6 * mf.M * 4;
+        p.PB = p.PL + 64 * mf.M * 4;
         p.agg = magg.as<uint64_t>();
         p.epoch = m_epoch;
         p.recompute = path_force == 3 ? 1 : 0;

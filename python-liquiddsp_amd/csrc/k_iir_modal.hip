@@ -2,29 +2,33 @@
 // execute_block, reference src/iirfilter.hpp:292-298 and :353) in ONE pass over
 // HBM, in modal coordinates.
 //
-// The host (capi.cpp, IirObj::modal_setup) diagonalises the filter's state-space
-// form s' = A s + B u, y = C s + D u: with A = V diag(lambda) V^-1 and V^-1 B = 1
-// the state z = V^-1 s evolves as one first-order complex recursion per pole,
-//     y_n = D u_n + sum_k Re(g_k z_k),      z_k <- lambda_k z_k + u_n
-// (a conjugate pole pair is one mode whose weight 2 is folded into g_k; each
-// component of the signal is real).  Every matrix of the chunked linear scan is
-// then diagonal.  A workgroup owns 2048 consecutive samples (the look-back
-// unit); each of its waves owns one component (I or Q), each lane a 32-sample
-// chunk of it:
-//  * the chunk ends, from a zero start, in L_k = sum_s lambda_k^(31 - s) u_s;
-//  * the wave's 64 chunks combine in a Kogge-Stone scan with lambda^(32 d);
+// The host (modal.cpp) diagonalises the filter's state-space form s' = A s +
+// B u, y = C s + D u into its modes (one per pole; a conjugate pair is one
+// mode for real input) and runs each mode as a real direct-form section -- the
+// parallel form of the filter:
+//     w_n = u_n - a1 w_{n-1} - a2 w_{n-2},   y_n = D u_n + sum_k c1 w_{n-1} + c2 w_{n-2}
+// (each component of the signal is real; a real pole is a first-order section,
+// a2 = c2 = 0).  The sections are independent, so every matrix of the chunked
+// linear scan is block-diagonal with 2 x 2 blocks A_k = [[-a1, -a2], [1, 0]].
+// A workgroup owns 2048 consecutive samples (the look-back unit); each of its
+// waves owns one component (I or Q), each lane a 32-sample chunk of it:
+//  * the chunk's end state from a zero start, L (the recursion, 2 FMAs per
+//    section and sample);
+//  * the wave's 64 chunks combine in a Kogge-Stone scan with A^(32 d);
 //  * the wave publishes the unit's end state from zero, BL_w, as {32-bit half,
-//    call epoch} granules with write-through stores, before it waits for
-//    anything (MI355X_MICROARCH.md: data-tagged 8-byte granules, sc1 stores and
-//    loads, no release/acquire fence);
+//    call epoch} granules, before it waits for anything; a reader takes a
+//    granule only when its tag is this call's epoch (MI355X_MICROARCH.md:
+//    data-tagged 8-byte granules, no release/acquire fence), so a stale line
+//    can delay a reader but never feed it old data;
 //  * its true start state is the look-back sum over the J units before it,
-//        S_w = sum_{i<J} lambda^(2048 i) BL_{w-1-i}  (+ lambda^(2048 w) S_call if w < J),
+//        S_w = sum_{i<J} A^(2048 i) BL_{w-1-i}  (+ A^(2048 w) S_call if w < J),
 //    exact to 2^-70 of the state (the host picks J from max |lambda|: older
 //    units contribute less than that).  A predecessor whose granules do not
 //    carry this call's epoch within the spin budget is recomputed from its input
 //    by the waiting wave -- the same instructions, so the same bits -- so no
 //    wave depends on the order in which the dispatcher starts workgroups;
-//  * every chunk re-runs from E_{t-1} + lambda^(32 t) S_w writing its outputs.
+//  * every chunk re-runs from E_{t-1} + A^(32 t) S_w writing its outputs
+//    (4 FMAs per section and sample).
 // The tile is loaded and stored coalesced through LDS (one plane per component);
 // the samples stay in LDS between the two passes, so HBM sees each sample read
 // once and written once (16 B per complex sample, 8 B real), against 24 B
@@ -50,8 +54,8 @@ constexpr uint64_t kSpinTicks = 5000;   // 50 us of s_memrealtime (100 MHz) befo
 static_assert(kC == 32, "the tile indexing below assumes 32-sample chunks");
 
 template <int M>
-struct Modal {
-    double r[M], i[M];
+struct Modal {            // per section: (w_n, w_{n-1})
+    double w0[M], w1[M];
 };
 
 typedef const double __attribute__((address_space(4)))* cdptr;   // uniform tables -> scalar loads
@@ -74,50 +78,96 @@ __device__ __forceinline__ float comp_at(const void* __restrict__ xv, long i, in
     else return ((const float*)xv)[NC * i + c];
 }
 
-// The unit's samples [wb, wb + 2048) into the LDS planes, plane c row t = chunk t
-// of component c; all NC x 64 threads, 64 consecutive samples per wave
-// instruction (zero past n).
-template <int NC, bool IQ16, bool FULL>
-__device__ __forceinline__ void tile_load(const void* __restrict__ xv, long n, long wb, int tid,
-                                          float (*__restrict__ pl)[64 * kRow])
+// Raw buffer access to the unit's samples: a descriptor over exactly the
+// samples of the call inside the unit (the hardware range check returns zeros
+// for loads past n and drops stores past n), per-lane 32-bit offsets and the
+// per-instruction step in soffset -- one address VGPR for the whole tile.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t unit_rsrc(const void* base, uint32_t bytes)
 {
-    constexpr int kQ = kUnit / (64 * NC);
-    if constexpr (NC == 2) {
-        using Raw = std::conditional_t<IQ16, int, float2>;
-        const Raw* __restrict__ xr = (const Raw*)xv;
-        Raw r[kQ];
-#pragma unroll
-        for (int q = 0; q < kQ; q++) {
-            const long gi = wb + tid + 128 * q;
-            if (FULL) r[q] = xr[gi];
-            else r[q] = gi < n ? xr[gi] : Raw{};
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+
+template <int S, bool VEC>   // S bytes per sample; VEC: 16-byte accesses, else one sample each
+struct Acc {
+    static constexpr int kP = VEC ? 16 / S : 1;       // samples per access
+    static constexpr int kW = kP * S / 4;             // dwords per access
+    static __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t so, uint32_t (&d)[kW])
+    {
+        if constexpr (kW == 4) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
+            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        } else if constexpr (kW == 2) {
+            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0);
+            d[0] = v.x, d[1] = v.y;
+        } else {
+            d[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0);
         }
+    }
+    static __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t so, const uint32_t (&d)[kW])
+    {
+        if constexpr (kW == 4) __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[0], d[1], d[2], d[3]}, rs, vo, so, 0);
+        else if constexpr (kW == 2) __builtin_amdgcn_raw_buffer_store_b64(u32x2{d[0], d[1]}, rs, vo, so, 0);
+        else __builtin_amdgcn_raw_buffer_store_b32(d[0], rs, vo, so, 0);
+    }
+};
+
+// The unit's samples into the LDS planes, plane c row t = chunk t of component
+// c; all NC x 64 threads, consecutive samples per lane and instruction.  VEC:
+// 16-byte loads (a whole unit, 16-byte aligned input), else one sample per load.
+template <int NC, bool IQ16, bool VEC>
+__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t rs, int tid, float (*__restrict__ pl)[64 * kRow])
+{
+    constexpr int S = IQ16 ? 4 : 4 * NC, T = 64 * NC;
+    using A = Acc<S, VEC>;
+    constexpr int kQ = kUnit / (T * A::kP);
+    static_assert((T * A::kP) % 32 == 0 && 32 % A::kP == 0, "whole rows per instruction");
+    uint32_t r[kQ][A::kW];
 #pragma unroll
-        for (int q = 0; q < kQ; q++) {
-            const int e = tid + 128 * q;
-            const int a = (e >> 5) * kRow + (e & 31);
+    for (int q = 0; q < kQ; q++) A::load(rs, (uint32_t)tid * A::kP * S, (uint32_t)q * T * A::kP * S, r[q]);
+    // sample e = (tid + T q) kP + j sits at row e / 32, column e % 32: a per-lane
+    // base plus constant offsets (immediate LDS offsets, no per-sample index math)
+    const int base = ((tid * A::kP) >> 5) * kRow + ((tid * A::kP) & 31);
+#pragma unroll
+    for (int q = 0; q < kQ; q++)
+#pragma unroll
+        for (int j = 0; j < A::kP; j++) {
+            const int a = base + (T * A::kP / 32) * kRow * q + j;
             if constexpr (IQ16) {
-                pl[0][a] = iq16_to_f((short)(r[q] & 0xffff));
-                pl[1][a] = iq16_to_f((short)(r[q] >> 16));
+                pl[0][a] = iq16_to_f((short)(r[q][j] & 0xffff));
+                pl[1][a] = iq16_to_f((short)(r[q][j] >> 16));
+            } else if constexpr (NC == 2) {
+                pl[0][a] = __uint_as_float(r[q][2 * j]);
+                pl[1][a] = __uint_as_float(r[q][2 * j + 1]);
             } else {
-                pl[0][a] = r[q].x;
-                pl[1][a] = r[q].y;
+                pl[0][a] = __uint_as_float(r[q][j]);
             }
         }
-    } else {
-        const float* __restrict__ xr = (const float*)xv;
-        float r[kQ];
+}
+
+// The unit's outputs from the LDS planes (complex or real float).
+template <int NC, bool VEC>
+__device__ __forceinline__ void tile_store(__amdgpu_buffer_rsrc_t rs, int tid, const float (*__restrict__ pl)[64 * kRow])
+{
+    constexpr int S = 4 * NC, T = 64 * NC;
+    using A = Acc<S, VEC>;
+    constexpr int kQ = kUnit / (T * A::kP);
+    const int base = ((tid * A::kP) >> 5) * kRow + ((tid * A::kP) & 31);
 #pragma unroll
-        for (int q = 0; q < kQ; q++) {
-            const long gi = wb + tid + 64 * q;
-            if (FULL) r[q] = xr[gi];
-            else r[q] = gi < n ? xr[gi] : 0.0f;
-        }
+    for (int q = 0; q < kQ; q++) {
+        uint32_t d[A::kW];
 #pragma unroll
-        for (int q = 0; q < kQ; q++) {
-            const int e = tid + 64 * q;
-            pl[0][(e >> 5) * kRow + (e & 31)] = r[q];
+        for (int j = 0; j < A::kP; j++) {
+            const int a = base + (T * A::kP / 32) * kRow * q + j;
+            if constexpr (NC == 2) {
+                d[2 * j] = __float_as_uint(pl[0][a]);
+                d[2 * j + 1] = __float_as_uint(pl[1][a]);
+            } else {
+                d[j] = __float_as_uint(pl[0][a]);
+            }
         }
+        A::store(rs, (uint32_t)tid * A::kP * S, (uint32_t)q * T * A::kP * S, d);
     }
 }
 
@@ -137,15 +187,13 @@ __device__ __forceinline__ void comp_load(const void* __restrict__ xv, long n, l
     wave_lds_sync();
 }
 
-// Pass 1 + the wave's inclusive scan: E_t = sum_{j <= t} lambda^(32 (t - j)) L_j
-// (lane 63: the unit's end state from a zero start).  L = sum_s lambda^(31-s) u_s
-// in pairs: Horner over the pairs with lambda^2, the pair sums u1 + lambda u0
-// (SGPR operands: lambda and lambda^2 only, so pass 1 and pass 2 keep their
-// coefficients in scalar registers), 3 FMAs per mode and sample.  One pair at a
-// time (sched_barrier): hoisting later samples' conversions ran out of VGPRs.
-// The scan powers are uniform: read through the constant address space they
-// are scalar loads.
-
+// Pass 1 + the wave's inclusive scan: E_t = sum_{j <= t} A^(32 (t - j)) L_j
+// (lane 63: the unit's end state from a zero start), L = the chunk's end state
+// from zero: per section w = u - a1 w1 - a2 w2, 2 FMAs per sample (a1, a2 as
+// SGPR operands).  One pair of samples at a time (sched_barrier): hoisting later
+// samples' conversions ran out of VGPRs.  The scan's 2 x 2 powers are uniform:
+// read through the constant address space they are scalar loads.
+typedef const double __attribute__((address_space(4)))* cdptr;
 
 template <int M>
 __device__ __forceinline__ void modal_scan(const IirModalCoef& cf, const double* __restrict__ PSg, const float (&u)[kC],
@@ -153,41 +201,43 @@ __device__ __forceinline__ void modal_scan(const IirModalCoef& cf, const double*
 {
     const cdptr PS = (cdptr)PSg;
 #pragma unroll
-    for (int k = 0; k < M; k++) E.r[k] = E.i[k] = 0.0;
+    for (int k = 0; k < M; k++) E.w0[k] = E.w1[k] = 0.0;
 #pragma unroll
     for (int g = 0; g < kC / 2; g++) {
-        const double u0 = (double)u[2 * g], u1 = (double)u[2 * g + 1];
 #pragma unroll
-        for (int k = 0; k < M; k++) {
-            const double pr = fma(cf.lr[k], u0, u1), pi = cf.li[k] * u0;     // u1 + lambda u0
-            const double er = E.r[k], ei = E.i[k];                            // E = lambda^2 E + pair
-            E.r[k] = fma(cf.l2r[k], er, fma(-cf.l2i[k], ei, pr));
-            E.i[k] = fma(cf.l2r[k], ei, fma(cf.l2i[k], er, pi));
+        for (int h = 0; h < 2; h++) {
+            const double ud = (double)u[2 * g + h];
+#pragma unroll
+            for (int k = 0; k < M; k++) {
+                const double w = fma(-cf.a1[k], E.w0[k], fma(-cf.a2[k], E.w1[k], ud));
+                E.w1[k] = E.w0[k];
+                E.w0[k] = w;
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int l = 0; l < 6; l++) {
         const int d = 1 << l;
-        const bool take = lane >= d;
 #pragma unroll
         for (int k = 0; k < M; k++) {
-            const double orr = __shfl_up(E.r[k], d), oi = __shfl_up(E.i[k], d);
-            const double ar = PS[(l * M + k) * 2], ai = PS[(l * M + k) * 2 + 1];
-            const double nr = fma(ar, orr, fma(-ai, oi, E.r[k]));
-            const double ni = fma(ar, oi, fma(ai, orr, E.i[k]));
-            E.r[k] = take ? nr : E.r[k];
-            E.i[k] = take ? ni : E.i[k];
+            const double o0 = __shfl_up(E.w0[k], d), o1 = __shfl_up(E.w1[k], d);
+            const double m00 = PS[(l * M + k) * 4], m01 = PS[(l * M + k) * 4 + 1];
+            const double m10 = PS[(l * M + k) * 4 + 2], m11 = PS[(l * M + k) * 4 + 3];
+            if (lane >= d) {
+                E.w0[k] = fma(m00, o0, fma(m01, o1, E.w0[k]));
+                E.w1[k] = fma(m10, o0, fma(m11, o1, E.w1[k]));
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-// Pass 2: the chunk from state z; row = this lane's samples in the LDS plane,
-// overwritten by the outputs (as float).  The output sum runs in two chains
-// (modes 0, 2, .. after D u; modes 1, 3, ..) so that no sample waits for a
-// serial chain of 2 M + 1 FMAs.  GUARD: the call ends inside this unit; the
-// state stops after sample cnt - 1.
+// Pass 2: the chunk from section states z; row = this lane's samples in the
+// LDS plane, overwritten by the outputs (as float).  The output sum runs in two
+// chains (sections 0, 2, .. after D u; sections 1, 3, ..) so that no sample
+// waits for a serial chain of 2 M + 1 FMAs.  GUARD: the call ends inside this
+// unit; the state stops after sample cnt - 1.
 template <int M, bool GUARD>
 __device__ __forceinline__ void modal_run(const IirModalCoef& cf, Modal<M>& z, float* __restrict__ row, int cnt)
 {
@@ -199,27 +249,25 @@ __device__ __forceinline__ void modal_run(const IirModalCoef& cf, Modal<M>& z, f
 #pragma unroll
         for (int k = 0; k < M; k++) {
             double& y = (k & 1) ? y1 : y0;
-            y = fma(cf.gr[k], z.r[k], y);
-            y = fma(-cf.gi[k], z.i[k], y);
-            const double nr = fma(cf.lr[k], z.r[k], fma(-cf.li[k], z.i[k], ud));
-            const double ni = fma(cf.li[k], z.r[k], cf.lr[k] * z.i[k]);
-            z.r[k] = on ? nr : z.r[k];
-            z.i[k] = on ? ni : z.i[k];
+            y = fma(cf.c1[k], z.w0[k], y);
+            y = fma(cf.c2[k], z.w1[k], y);
+            const double w = fma(-cf.a1[k], z.w0[k], fma(-cf.a2[k], z.w1[k], ud));
+            z.w1[k] = on ? z.w0[k] : z.w1[k];
+            z.w0[k] = on ? w : z.w0[k];
         }
         row[s] = (float)(y0 + y1);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-// t += pw (x) a per mode (complex product, pw = [M][re, im])
+// t += P_k a per section (P = [M][2 x 2], row-major)
 template <int M>
-__device__ __forceinline__ void add_pow(const double* __restrict__ pw, const Modal<M>& a, Modal<M>& t)
+__device__ __forceinline__ void add_mat(const double* __restrict__ P, const Modal<M>& a, Modal<M>& t)
 {
 #pragma unroll
     for (int k = 0; k < M; k++) {
-        const double pr = pw[2 * k], pi = pw[2 * k + 1];
-        t.r[k] = fma(pr, a.r[k], fma(-pi, a.i[k], t.r[k]));
-        t.i[k] = fma(pr, a.i[k], fma(pi, a.r[k], t.i[k]));
+        t.w0[k] = fma(P[4 * k], a.w0[k], fma(P[4 * k + 1], a.w1[k], t.w0[k]));
+        t.w1[k] = fma(P[4 * k + 2], a.w0[k], fma(P[4 * k + 3], a.w1[k], t.w1[k]));
     }
 }
 
@@ -236,11 +284,25 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int c = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave's component (wave-uniform)
-    const long w = blockIdx.x;
+    // XCD-aware unit order: blocks b, b + 8, b + 16, .. share an XCD (observed
+    // round-robin placement, MI355X_MICROARCH.md -- used for speed only) and take
+    // one contiguous range of units each, so a unit's predecessors were published
+    // into the same L2 (plain stores, read back with L2-served sc1 loads).  The
+    // first J units of a range need units of another range: those recompute them.
+    const long xq = blockIdx.x & 7, xi = blockIdx.x >> 3;
+    long range0 = 0;
+    for (long y = 0; y < xq; y++) range0 += (nw - y + 7) >> 3;
+    const long w = range0 + xi;
     const long wb = w * kUnit;
     const bool full = wb + kUnit <= n;
-    if (full) tile_load<NC, IQ16, true>(xv, n, wb, tid, pl);
-    else tile_load<NC, IQ16, false>(xv, n, wb, tid, pl);
+    constexpr int kSin = IQ16 ? 4 : 4 * NC, kSout = 4 * NC;
+    const uint32_t cnt = (uint32_t)min((long)kUnit, n - wb);   // samples of the call in this unit
+    const bool vec = full && (((uintptr_t)xv | (uintptr_t)yv) & 15) == 0;
+    {
+        const __amdgpu_buffer_rsrc_t rx = unit_rsrc((const char*)xv + wb * kSin, cnt * kSin);
+        if (vec) tile_load<NC, IQ16, true>(rx, tid, pl);
+        else tile_load<NC, IQ16, false>(rx, tid, pl);
+    }
     __syncthreads();
     float* row = pl[c] + lane * kRow;  // this lane's chunk of its component: input, then output
     float u[kC];                        // pass 1 only; pass 2 reads the plane again
@@ -250,7 +312,7 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
     Modal<M> E;
 #ifdef LDSP_TUNING
     if (p.variant & 4)
-        for (int k = 0; k < M; k++) E.r[k] = E.i[k] = u[k];
+        for (int k = 0; k < M; k++) E.w0[k] = E.w1[k] = u[k];
     else
 #endif
     modal_scan<M>(cf, p.PS, u, lane, E);
@@ -261,41 +323,40 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
         const uint64_t tag = (uint64_t)p.epoch << 32;
 #pragma unroll
         for (int k = 0; k < M; k++) {
-            const uint64_t br = __builtin_bit_cast(uint64_t, E.r[k]), bi = __builtin_bit_cast(uint64_t, E.i[k]);
-            __hip_atomic_store(g + 4 * k + 0, tag | (uint32_t)br, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g + 4 * k + 1, tag | (uint32_t)(br >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g + 4 * k + 2, tag | (uint32_t)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g + 4 * k + 3, tag | (uint32_t)(bi >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t br = __builtin_bit_cast(uint64_t, E.w0[k]), bi = __builtin_bit_cast(uint64_t, E.w1[k]);
+            g[4 * k + 0] = tag | (uint32_t)br;
+            g[4 * k + 1] = tag | (uint32_t)(br >> 32);
+            g[4 * k + 2] = tag | (uint32_t)bi;
+            g[4 * k + 3] = tag | (uint32_t)(bi >> 32);
         }
     }
     // this lane's exclusive prefix E_{t-1}
     Modal<M> z;
 #pragma unroll
     for (int k = 0; k < M; k++) {
-        const double er = __shfl_up(E.r[k], 1), ei = __shfl_up(E.i[k], 1);
-        z.r[k] = lane == 0 ? 0.0 : er;
-        z.i[k] = lane == 0 ? 0.0 : ei;
+        const double er = __shfl_up(E.w0[k], 1), ei = __shfl_up(E.w1[k], 1);
+        z.w0[k] = lane == 0 ? 0.0 : er;
+        z.w1[k] = lane == 0 ? 0.0 : ei;
     }
 
-    // look-back: lane i < jw holds lambda^(2048 i) x (BL_{w-1-i}, or S_call when i == w)
+    // look-back: lane i < jw fetches BL_{w-1-i} (S_call when i == w)
 #ifdef LDSP_TUNING
     const int jw = (p.variant & 1) ? 0 : (int)min((long)p.J, w + 1);
 #else
     const int jw = (int)min((long)p.J, w + 1);
 #endif
-    Modal<M> term;
+    Modal<M> a;                         // lane i < jw: predecessor i's state
 #pragma unroll
-    for (int k = 0; k < M; k++) term.r[k] = term.i[k] = 0.0;
+    for (int k = 0; k < M; k++) a.w0[k] = a.w1[k] = 0.0;
     bool need = false;
     if (lane < jw) {
-        Modal<M> a;
         if (lane == w) {
 #pragma unroll
             for (int k = 0; k < M; k++) {
-                a.r[k] = st_in[(c * M + k) * 2];
-                a.i[k] = st_in[(c * M + k) * 2 + 1];
+                a.w0[k] = st_in[(c * M + k) * 2];
+                a.w1[k] = st_in[(c * M + k) * 2 + 1];
             }
-        } else if (p.recompute) {
+        } else if (p.recompute || w - 1 - lane < range0) {   // test hook, or a unit of another XCD's range
             need = true;
         } else {
             const uint64_t* g = p.agg + ((w - 1 - lane) * NC + c) * kGran;
@@ -311,8 +372,8 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
                     const uint64_t g3 = __hip_atomic_load(g + 4 * k + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     bad |= ((uint32_t)(g0 >> 32) ^ p.epoch) | ((uint32_t)(g1 >> 32) ^ p.epoch) |
                            ((uint32_t)(g2 >> 32) ^ p.epoch) | ((uint32_t)(g3 >> 32) ^ p.epoch);
-                    a.r[k] = __builtin_bit_cast(double, (g1 << 32) | (uint32_t)g0);
-                    a.i[k] = __builtin_bit_cast(double, (g3 << 32) | (uint32_t)g2);
+                    a.w0[k] = __builtin_bit_cast(double, (g1 << 32) | (uint32_t)g0);
+                    a.w1[k] = __builtin_bit_cast(double, (g3 << 32) | (uint32_t)g2);
                 }
                 ok = bad == 0;
                 if (ok || wall_clock64() - t0 > kSpinTicks) break;
@@ -320,7 +381,6 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
             }
             need = !ok;
         }
-        if (!need) add_pow<M>(p.PB + (size_t)lane * M * 2, a, term);
     }
     // predecessors not seen in time: recompute their end states here (the
     // plane is the scratch; this wave's own input is reloaded afterwards)
@@ -334,31 +394,37 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
             for (int s = 0; s < kC; s++) u[s] = row[s];
             Modal<M> Eo;
             modal_scan<M>(cf, p.PS, u, lane, Eo);
-            Modal<M> a;
 #pragma unroll
             for (int k = 0; k < M; k++) {
-                a.r[k] = rl_f64(Eo.r[k], 63);
-                a.i[k] = rl_f64(Eo.i[k], 63);
+                const double e0 = rl_f64(Eo.w0[k], 63), e1 = rl_f64(Eo.w1[k], 63);
+                if (lane == i) {
+                    a.w0[k] = e0;
+                    a.w1[k] = e1;
+                }
             }
-            if (lane == i) add_pow<M>(p.PB + (size_t)i * M * 2, a, term);
         }
         comp_load<NC, IQ16>(xv, n, w, lane, c, pl[c]);
     }
-    // S_w = sum of the terms in lane order; chunk start = E_{t-1} + lambda^(32 t) S_w
+    // S_w = sum_i A^(2048 i) a_i, in order of i, on wave-uniform values (the
+    // predecessors' states read lane by lane, the powers as scalar loads);
+    // chunk start = E_{t-1} + A^(32 t) S_w
+    const cdptr PB = (cdptr)p.PB;
     Modal<M> S;
 #pragma unroll
-    for (int k = 0; k < M; k++) S.r[k] = S.i[k] = 0.0;
+    for (int k = 0; k < M; k++) S.w0[k] = S.w1[k] = 0.0;
     for (int i = 0; i < jw; i++)
 #pragma unroll
         for (int k = 0; k < M; k++) {
-            S.r[k] += rl_f64(term.r[k], i);
-            S.i[k] += rl_f64(term.i[k], i);
+            const double a0 = rl_f64(a.w0[k], i), a1 = rl_f64(a.w1[k], i);
+            const int q = (i * M + k) * 4;
+            S.w0[k] = fma(PB[q], a0, fma(PB[q + 1], a1, S.w0[k]));
+            S.w1[k] = fma(PB[q + 2], a0, fma(PB[q + 3], a1, S.w1[k]));
         }
-    add_pow<M>(p.PL + (size_t)lane * M * 2, S, z);
+    add_mat<M>(p.PL + (size_t)lane * M * 4, S, z);
 
     const long rem = n - (wb + (long)lane * kC);
 #ifdef LDSP_TUNING
-    if (p.variant & 2) row[0] += (float)z.r[0];
+    if (p.variant & 2) row[0] += (float)z.w0[0];
     else
 #endif
     if (full) modal_run<M, false>(cf, z, row, kC);
@@ -366,21 +432,13 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
     if (rem > 0 && rem <= kC)            // the chunk holding sample n - 1: the call's end state
 #pragma unroll
         for (int k = 0; k < M; k++) {
-            st_out[(c * M + k) * 2] = z.r[k];
-            st_out[(c * M + k) * 2 + 1] = z.i[k];
+            st_out[(c * M + k) * 2] = z.w0[k];
+            st_out[(c * M + k) * 2 + 1] = z.w1[k];
         }
     __syncthreads();
-    constexpr int kQ = kUnit / (64 * NC);
-#pragma unroll
-    for (int q = 0; q < kQ; q++) {
-        const int e = tid + 64 * NC * q;
-        const int a = (e >> 5) * kRow + (e & 31);
-        const long gi = wb + e;
-        if (full || gi < n) {
-            if constexpr (NC == 2) ((float2*)yv)[gi] = make_float2(pl[0][a], pl[1][a]);
-            else yv[gi] = pl[0][a];
-        }
-    }
+    const __amdgpu_buffer_rsrc_t ry = unit_rsrc((const char*)yv + wb * kSout, cnt * kSout);
+    if (vec) tile_store<NC, true>(ry, tid, pl);
+    else tile_store<NC, false>(ry, tid, pl);
 }
 
 template <int NC, int M, bool IQ16>

@@ -113,26 +113,26 @@ struct IirBlkPlan {
 void iir_blk(bool cplx, const IirDesc& d, const float* hb, const float* ha, const void* x, size_t n, double* state64,
              const IirBlkPlan& p, void* y, hipStream_t s, bool iq16 = false);
 // Single-pass float64 scan in modal coordinates (k_iir_modal.hip): the filter
-// as M <= 8 first-order complex modes, z_k <- lambda_k z_k + u, y = d u +
-// sum_k Re(g_k z_k) (pair weights folded into g).  One wave = 64 chunks of
-// kIirModalChunk samples; each wave's start state is the look-back sum over the
-// J <= kIirModalJmax waves before it (valid when max|lambda|^(2048 J) < 2^-70).
-// State layout (st_in / st_out, distinct buffers): double [ncomp][M][re, im].
+// as M <= 8 parallel sections (one per pole pair or real pole) in direct form,
+// w_n = u_n - a1 w_{n-1} - a2 w_{n-2}, y = d u + sum_k c1 w_{n-1} + c2 w_{n-2}
+// (modal.hpp).  One wave = 64 chunks of kIirModalChunk samples; each unit's
+// start state is the look-back sum over the J <= kIirModalJmax units before it
+// (valid when max|lambda|^(2048 J) < 2^-70).  State layout (st_in / st_out,
+// distinct buffers): double [ncomp][M][w_n, w_{n-1}].
 constexpr int kIirModalMax = 8;
 constexpr int kIirModalChunk = 32;
 constexpr int kIirModalJmax = 64;
 struct IirModalCoef {     // kernel argument
     int M;
-    double lr[kIirModalMax], li[kIirModalMax];   // lambda_k
-    double gr[kIirModalMax], gi[kIirModalMax];   // g_k (x2 for a conjugate pair)
-    double l2r[kIirModalMax], l2i[kIirModalMax];  // lambda_k^2
+    double a1[kIirModalMax], a2[kIirModalMax];   // section denominators
+    double c1[kIirModalMax], c2[kIirModalMax];   // section outputs
     double d;                                    // direct term
 };
 struct IirModalPlan {
-    int J;                // look-back depth (waves)
-    const double* PS;     // [6][M][re, im]   lambda^(32 * 2^l), l = 0..5
-    const double* PL;     // [64][M][re, im]  lambda^(32 t), t = lane
-    const double* PB;     // [J][M][re, im]   lambda^(2048 i)
+    int J;                // look-back depth (units)
+    const double* PS;     // [6][M][4]   A_k^(32 * 2^l), l = 0..5 (2 x 2, row-major)
+    const double* PL;     // [64][M][4]  A_k^(32 t), t = lane
+    const double* PB;     // [J][M][4]   A_k^(2048 i)
     uint64_t* agg;        // [nunits][ncomp][M * 4] {32-bit half, epoch} granules (zeroed when allocated)
     uint32_t epoch;       // per call, never 0
     int recompute = 0;    // test hook: every wave recomputes its predecessors instead of reading them

@@ -7,7 +7,9 @@
 //     z_k' = lambda_k z_k + u,    y = Dd u + sum_k g_k z_k.
 // For a real filter the non-real poles come in conjugate pairs whose modes are
 // conjugate for real input: one mode per pair carries weight 2 (y gets
-// 2 Re(g_k z_k)), a real pole one mode of weight 1.  The form is accepted only
+// 2 Re(g_k z_k)), a real pole one mode of weight 1.  The kernel runs each mode
+// as a real direct-form section (below: the parallel form of the filter, one
+// section per pole pair).  The form is accepted only
 // when it reproduces the long-double state-space recursion to 1e-10 (impulse +
 // noise input, the free response of a random state, and the state round trip);
 // clustered poles (narrow high-order Butterworth / Chebyshev-I designs) make V
@@ -243,48 +245,64 @@ ModalForm modal_form(int D, const std::vector<ld>& A, const std::vector<ld>& B, 
     if (M > k::kIirModalMax) return fail("too many modes");
     f.M = M;
 
+    // Each mode as a real second-order section (a real pole: first order) in
+    // direct form: w_n = u_n - a1 w_{n-1} - a2 w_{n-2}, section state
+    // v = (w_n, w_{n-1}), output c1 w_{n-1} + c2 w_{n-2}.  For a pair,
+    // 1 / (1 - lambda z^-1) = (1 - conj(lambda) z^-1) / ((1 - lambda z^-1)(1 - conj(lambda) z^-1)),
+    // so z_n = w_n - conj(lambda) w_{n-1}, and 2 Re(g z_{n-1}) = c1 w_{n-1} + c2 w_{n-2}
+    // with c1 = 2 Re g, c2 = -2 Re(g conj(lambda)): 4 FMAs per section and
+    // sample instead of the 6 of the complex recursion.
     f.cf = k::IirModalCoef{};
     f.cf.M = M;
     f.cf.d = (double)Dd;
-    std::vector<cld> lam(M), gw(M);
+    std::vector<ld> A11(M), A12(M);    // section matrix [[A11, A12], [1, 0]] = [[-a1, -a2], [1, 0]] (double-rounded)
     for (int m = 0; m < M; m++) {
         const int k = rep[m];
         const bool real = wt[m] == 1;
-        lam[m] = real ? cld(poles[k].real(), 0) : poles[k];
-        gw[m] = (ld)wt[m] * (real ? cld(g[k].real(), 0) : g[k]);
-        const cld l2 = lam[m] * lam[m];
-        f.cf.lr[m] = (double)lam[m].real();
-        f.cf.li[m] = (double)lam[m].imag();
-        f.cf.gr[m] = (double)gw[m].real();
-        f.cf.gi[m] = (double)gw[m].imag();
-        f.cf.l2r[m] = (double)l2.real();
-        f.cf.l2i[m] = (double)l2.imag();
+        const cld lam = real ? cld(poles[k].real(), 0) : poles[k];
+        const cld gk = real ? cld(g[k].real(), 0) : g[k];
+        f.cf.a1[m] = (double)(real ? -lam.real() : -2 * lam.real());
+        f.cf.a2[m] = (double)(real ? 0 : std::norm(lam));
+        f.cf.c1[m] = (double)(real ? gk.real() : 2 * gk.real());
+        f.cf.c2[m] = (double)(real ? 0 : -2 * (gk.real() * lam.real() + gk.imag() * lam.imag()));
+        A11[m] = -(ld)f.cf.a1[m];
+        A12[m] = -(ld)f.cf.a2[m];
     }
-    f.to_s.assign((size_t)D * M, 0);
-    f.to_z.assign((size_t)M * D, 0);
+    // state conversions: DF-II layout s (D) <-> section states v (2 M)
+    f.to_v.assign((size_t)2 * M * D, 0.0);
+    f.from_v.assign((size_t)D * 2 * M, 0.0);
     for (int m = 0; m < M; m++) {
         const int k = rep[m];
         const bool real = wt[m] == 1;
+        const ld lr = poles[k].real(), li = real ? 0 : poles[k].imag();
         for (int i = 0; i < D; i++) {
-            const cld v = (ld)wt[m] * V[i * D + k];
-            f.to_s[(size_t)i * M + m] = std::complex<double>((double)v.real(), real ? 0.0 : (double)v.imag());
-            const cld r = Vi[k * D + i];
-            f.to_z[(size_t)m * D + i] = std::complex<double>((double)r.real(), real ? 0.0 : (double)r.imag());
+            const cld r = Vi[k * D + i];                 // z_m = sum_i r s_i
+            const cld v = V[i * D + k];                  // s_i gets wt Re(v z_m)
+            if (real) {
+                f.to_v[(size_t)(2 * m) * D + i] = (double)r.real();
+                f.from_v[(size_t)i * 2 * M + 2 * m] = (double)v.real();
+            } else {                                     // v1 = Im z / li, v0 = Re z + lr v1
+                f.to_v[(size_t)(2 * m + 1) * D + i] = (double)(r.imag() / li);
+                f.to_v[(size_t)(2 * m) * D + i] = (double)(r.real() + lr * r.imag() / li);
+                f.from_v[(size_t)i * 2 * M + 2 * m] = (double)(2 * v.real());
+                f.from_v[(size_t)i * 2 * M + 2 * m + 1] = (double)(-2 * (v.real() * lr + v.imag() * li));
+            }
         }
     }
 
-    // host check: the double-precision modal recursion (the kernel's formulas)
-    // against the long-double state-space recursion
-    auto modal_step = [&](std::vector<std::complex<double>>& z, double u) {
-        double y = f.cf.d * u;
+    // host check: the double-precision section recursion (the kernel's
+    // formulas and summation order) against the long-double state-space recursion
+    auto sec_step = [&](std::vector<double>& v, double u) {
+        double y0 = f.cf.d * u, y1 = 0.0;
         for (int m = 0; m < M; m++) {
-            y = std::fma(f.cf.gr[m], z[m].real(), y);
-            y = std::fma(-f.cf.gi[m], z[m].imag(), y);
-            const double nr = std::fma(f.cf.lr[m], z[m].real(), std::fma(-f.cf.li[m], z[m].imag(), u));
-            const double ni = std::fma(f.cf.li[m], z[m].real(), f.cf.lr[m] * z[m].imag());
-            z[m] = std::complex<double>(nr, ni);
+            double& y = (m & 1) ? y1 : y0;
+            y = std::fma(f.cf.c1[m], v[2 * m], y);
+            y = std::fma(f.cf.c2[m], v[2 * m + 1], y);
+            const double w = std::fma(-f.cf.a1[m], v[2 * m], std::fma(-f.cf.a2[m], v[2 * m + 1], u));
+            v[2 * m + 1] = v[2 * m];
+            v[2 * m] = w;
         }
-        return y;
+        return y0 + y1;
     };
     auto ss_step = [&](std::vector<ld>& s, ld u) {
         ld y = Dd * u;
@@ -301,13 +319,13 @@ ModalForm modal_form(int D, const std::vector<ld>& A, const std::vector<ld>& B, 
     Lcg rng;
     double err = 0;
     {   // impulse + noise from rest
-        std::vector<std::complex<double>> z(M, 0.0);
+        std::vector<double> v(2 * M, 0.0);
         std::vector<ld> s(D, 0);
         double ymax = 0, dmax = 0;
         for (int n = 0; n < 4096; n++) {
             const double u = n == 0 ? 1.0 : rng.next();
             const ld ys = ss_step(s, u);
-            const double ym = modal_step(z, u);
+            const double ym = sec_step(v, u);
             ymax = std::max(ymax, (double)std::fabs(ys));
             dmax = std::max(dmax, std::fabs(ym - (double)ys));
         }
@@ -320,21 +338,21 @@ ModalForm modal_form(int D, const std::vector<ld>& A, const std::vector<ld>& B, 
             s[i] = rng.next();
             smax = std::max(smax, (double)std::fabs(s[i]));
         }
-        std::vector<std::complex<double>> z(M, 0.0);
-        for (int m = 0; m < M; m++)
-            for (int i = 0; i < D; i++) z[m] += f.to_z[(size_t)m * D + i] * (double)s[i];
+        std::vector<double> v(2 * M, 0.0);
+        for (int q = 0; q < 2 * M; q++)
+            for (int i = 0; i < D; i++) v[q] += f.to_v[(size_t)q * D + i] * (double)s[i];
         double dmax = 0;
         for (int i = 0; i < D; i++) {
-            double v = 0;
-            for (int m = 0; m < M; m++) v += (f.to_s[(size_t)i * M + m] * z[m]).real();
-            dmax = std::max(dmax, std::fabs(v - (double)s[i]));
+            double t = 0;
+            for (int q = 0; q < 2 * M; q++) t += f.from_v[(size_t)i * 2 * M + q] * v[q];
+            dmax = std::max(dmax, std::fabs(t - (double)s[i]));
         }
         err = std::max(err, dmax / smax);
         double ymax = 0;
         dmax = 0;
         for (int n = 0; n < 512; n++) {
             const ld ys = ss_step(s, 0);
-            const double ym = modal_step(z, 0.0);
+            const double ym = sec_step(v, 0.0);
             ymax = std::max(ymax, (double)std::fabs(ys));
             dmax = std::max(dmax, std::fabs(ym - (double)ys));
         }
@@ -352,17 +370,29 @@ ModalForm modal_form(int D, const std::vector<ld>& A, const std::vector<ld>& B, 
     if (J > k::kIirModalJmax) return fail("decays too slowly for the look-back");
     f.J = J;
 
-    f.tables.clear();
-    auto put = [&](cld v) {
-        f.tables.push_back((double)v.real());
-        f.tables.push_back((double)v.imag());
+    // powers of the section matrices, [m00, m01, m10, m11] per section
+    auto matpow2 = [&](int m, unsigned long long e) {
+        ld r[4] = {1, 0, 0, 1}, b[4] = {A11[m], A12[m], 1, 0};
+        while (e) {
+            if (e & 1) {
+                const ld t[4] = {r[0] * b[0] + r[1] * b[2], r[0] * b[1] + r[1] * b[3], r[2] * b[0] + r[3] * b[2],
+                                 r[2] * b[1] + r[3] * b[3]};
+                std::copy(t, t + 4, r);
+            }
+            const ld t[4] = {b[0] * b[0] + b[1] * b[2], b[0] * b[1] + b[1] * b[3], b[2] * b[0] + b[3] * b[2],
+                             b[2] * b[1] + b[3] * b[3]};
+            std::copy(t, t + 4, b);
+            e >>= 1;
+        }
+        for (int q = 0; q < 4; q++) f.tables.push_back((double)r[q]);
     };
+    f.tables.clear();
     for (int l = 0; l < 6; l++)
-        for (int m = 0; m < M; m++) put(cpow_u(lam[m], (unsigned long long)k::kIirModalChunk << l));
+        for (int m = 0; m < M; m++) matpow2(m, (unsigned long long)k::kIirModalChunk << l);
     for (int t = 0; t < 64; t++)
-        for (int m = 0; m < M; m++) put(cpow_u(lam[m], (unsigned long long)k::kIirModalChunk * t));
+        for (int m = 0; m < M; m++) matpow2(m, (unsigned long long)k::kIirModalChunk * t);
     for (int i = 0; i < J; i++)
-        for (int m = 0; m < M; m++) put(cpow_u(lam[m], (unsigned long long)k::kIirModalChunk * 64 * i));
+        for (int m = 0; m < M; m++) matpow2(m, (unsigned long long)k::kIirModalChunk * 64 * i);
     f.ok = true;
     return f;
 }

@@ -17,11 +17,11 @@ struct ModalForm {
     int D = 0, M = 0, J = 0;
     double err = 0.0;             // host check: max |y_modal - y_ss| / max |y_ss| (impulse, noise, free response)
     k::IirModalCoef cf{};
-    std::vector<double> tables;   // PS [6][M][2] | PL [64][M][2] | PB [J][M][2]  (k::IirModalPlan)
+    std::vector<double> tables;   // PS [6][M][4] | PL [64][M][4] | PB [J][M][4]  (k::IirModalPlan)
     // state conversions between the DF-II layout of the scans (s, D reals per
-    // component) and the modes: s = Re(sum_k to_s[i*M+k] z_k) (pair weight
-    // folded in), z_k = sum_i to_z[k*D+i] s_i
-    std::vector<std::complex<double>> to_s, to_z;
+    // component) and the section states v (2 M reals: w_n, w_{n-1} per
+    // section): v = to_v s ([2M][D]), s = from_v v ([D][2M])
+    std::vector<double> to_v, from_v;
 };
 
 // s' = A s + B u, y = C s + Dd u (A row-major D x D); poles = the D eigenvalues of A
