@@ -537,7 +537,7 @@ def components(L, device, reps=5):
     return out
 
 
-def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2):
+def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False):
     """SURVEY 8(e)'s caveat: independent channels also share one GPU -- each
     channel's serial PLL walk / AGC repair occupy one CU, so C channels on C
     stream pairs overlap.  Aggregate IQ Msamples/s of `channels` AMRadio chains
@@ -545,16 +545,33 @@ def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2):
     xs = [synth_channel(n, r, device) for r in range(channels)]
     radios = [AMRadio(L) for _ in range(channels)]
     strm = [[torch.cuda.Stream(device) for _ in range(per)] for _ in range(channels)]
+    # split: the front stages (IIR, resampler, AGC) and the back stages (AmpModem,
+    # de-emphasis) of a step on different streams, so that stream order never
+    # holds a step's front behind an earlier step's walk
+    back = [[torch.cuda.Stream(device) for _ in range(per)] for _ in range(channels)] if split else None
 
     def step(k, w=None):
         kk = k if k is not None else w
         for c in range(channels):
+            if not split:
+                with torch.cuda.stream(strm[c][kk % per]):
+                    radios[c](xs[c])
+                continue
+            r = radios[c]
             with torch.cuda.stream(strm[c][kk % per]):
-                radios[c](xs[c])
+                a = r.agc(r.resample(r.bandpass(xs[c])))
+                ev = torch.cuda.Event()
+                ev.record()
+            with torch.cuda.stream(back[c][kk % per]):
+                torch.cuda.current_stream().wait_event(ev)
+                r.audio_filter(r.am(a))
 
-    t = timed_steps(step, steps, 2, torch.cuda.synchronize, lambda: None)
+    # warm-up steps cover every stream (torch's caching allocator maps fresh blocks
+    # for a stream's first use, which must not land in the timed steps)
+    t = timed_steps(step, steps, max(2, per), torch.cuda.synchronize, lambda: None)
     del xs
-    return {"channels": channels, "streams_per_channel": per, "steps": steps, "ms_per_step": round(t / steps * 1e3, 3),
+    return {"channels": channels, "streams_per_channel": per * (2 if split else 1), "split_front_back": split,
+            "steps": steps, "ms_per_step": round(t / steps * 1e3, 3),
             "Msamples_s": round(channels * n * steps / t / 1e6, 1),
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")}
 

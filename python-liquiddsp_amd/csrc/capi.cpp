@@ -1834,7 +1834,13 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             p.W = tsa ? 0 : W;                 // tsa: every chunk from 1 on is checked against its predecessor
             p.Wa = Wa;
             p.rounds = tsa ? 1 : std::max(0, std::min(rounds, 6));   // tsa: one run covers the rare deviation
-            p.C = 256;
+            // chunk length: every chunk re-runs Wa + W warm-up steps (6 000 at
+            // bandwidth 0.01) for its C outputs, so C = 1024 does a quarter of the
+            // front's work of C = 256 at ~20 % more latency (hidden under the PLL
+            // walk in a streamed chain); measured on 8 channels per GPU 6.6 -> 6.3
+            // ms per step (scripts/agc_chunk_sweep.sh).  Small calls (tsa) keep 256.
+            static const int agc_c = LDSP_KNOB("LDSP_AGC_C", 1024);
+            p.C = tsa ? 256 : agc_c;
             p.nchunks = (long)((n + p.C - 1) / p.C);
             p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks), q->device);
             p.hist = q->hist[h3].p;
