@@ -427,9 +427,13 @@ PMC, PMC_SOURCE = _pmc_summary()
 
 
 def pmc_traffic(run, kernel):
+    """HBM bytes per launch of `kernel` (a profiling label; the rocprof name may
+    carry a variant suffix, e.g. k_fir_fft512x for the k_fir_fft512 label)."""
     try:
-        return round(PMC[run][kernel]["hbm_bytes"])
-    except (TypeError, KeyError):
+        d = PMC[run]
+        k = kernel if kernel in d else next(n for n in sorted(d) if n.startswith(kernel))
+        return round(d[k]["hbm_bytes"])
+    except (TypeError, KeyError, StopIteration):
         return None
 
 

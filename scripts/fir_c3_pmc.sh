@@ -1,10 +1,11 @@
 #!/bin/bash
-# BASELINE config 3 (NCO.mix_down + 255-tap FIR, 256 Mi) fused kernel alone:
+# BASELINE config 3 (NCO.mix_down + 255-tap FIR, 256 Mi) fused kernel alone (or
+# another firbench workload: FIRBENCH_* and PMC_OUT):
 # kernel-trace stats, HBM bytes (FETCH_SIZE x2 per the gfx950 correction,
 # WRITE_SIZE) and SQ / GRBM counters, each in its own rocprofv3 pass.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-export TMPDIR=/tmp FIRBENCH_TAPS=${FIRBENCH_TAPS:-255} FIRBENCH_N=${FIRBENCH_N:-1048576} FIRBENCH_REPS=${FIRBENCH_REPS:-6} FIRBENCH_C3=1
-out=gpurun_out/c3pmc; mkdir -p $out
+export TMPDIR=/tmp FIRBENCH_TAPS=${FIRBENCH_TAPS:-255} FIRBENCH_N=${FIRBENCH_N:-1048576} FIRBENCH_REPS=${FIRBENCH_REPS:-6} FIRBENCH_C3=${FIRBENCH_C3:-1}
+out=${PMC_OUT:-gpurun_out/c3pmc}; mkdir -p $out
 F="python3 scripts/firbench.py"
 run() { local name=$1; shift; timeout -s KILL 120 rocprofv3 "$@" > $out/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $out/$name.log; exit $rc; }; }
 run trace --kernel-trace --stats --output-format csv -d $out/trace -o c3 -- $F
