@@ -226,6 +226,13 @@ int ldsp_iirfilt_execute_iq16(ldsp_iirfilt_t q, const void *x, size_t n, void *y
  * ---------------------------------------------------------------------- */
 typedef struct ldsp_agc_s *ldsp_agc_t;
 int ldsp_agc_create(ldsp_agc_t *q);
+/* Test hook: small AGC calls (the one-wave chunk path, 320 <= n < the
+ * chunk-parallel threshold) start every chunk but the first 1 ulp away from its
+ * approximated state, so the in-kernel check re-runs each of them from its
+ * predecessor's end state; the output stays bit-identical to agc_crcf. */
+int ldsp_debug_agc_tsa_perturb(ldsp_agc_t q, int on);
+/* chunks re-run by that in-kernel check since the object was created */
+int ldsp_debug_agc_tsa_reruns(ldsp_agc_t q, unsigned int *count);
 int ldsp_agc_destroy(ldsp_agc_t q);
 int ldsp_agc_reset(ldsp_agc_t q);
 int ldsp_agc_set_bandwidth(ldsp_agc_t q, float bw);

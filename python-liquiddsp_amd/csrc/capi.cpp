@@ -592,6 +592,10 @@ struct IirObj {
         p.agg = magg.as<uint64_t>();
         p.epoch = m_epoch;
         p.recompute = path_force == 3 ? 1 : 0;
+        // one XCD while its 32 CUs stream the call faster than a range start
+        // recomputes its J predecessors (~2.5 us each): up to 16 J units
+        static const int onex = LDSP_KNOB("LDSP_IIR_ONEXCD", -1);
+        p.one_xcd = onex >= 0 ? onex : (units <= 16L * mf.J ? 1 : 0);
         p.variant = LDSP_KNOB("LDSP_IIR_VARIANT", 0);
         return p;
     }
@@ -651,6 +655,7 @@ struct AgcObj {
     // state), front = front halves (history), slot[s] = scratch slot s free.
     StreamMark ord, front, slot[2];
     Staging stg;
+    int tsa_perturb = 0;              // ldsp_debug_agc_tsa_perturb (test hook)
     void init()
     {
         // agc_crcf_create: bandwidth 0.01, reset (g=1, y2'=1), squelch disabled,
@@ -1517,6 +1522,22 @@ int ldsp_debug_iir_path(ldsp_iirfilt_t q, int path)
         q->path_force = path;
     });
 }
+int ldsp_debug_agc_tsa_perturb(ldsp_agc_t q, int on)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->tsa_perturb = on ? 1 : 0;
+    });
+}
+int ldsp_debug_agc_tsa_reruns(ldsp_agc_t q, unsigned int* count)
+{
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(count);
+        q->pull();
+        *count = (unsigned)q->h.pad[0];
+    });
+}
 int ldsp_debug_iir_modal_info(ldsp_iirfilt_t q, int* ok, int* modes, int* lookback, double* err)
 {
     return guard([&] {
@@ -1845,7 +1866,11 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks), q->device);
             p.hist = q->hist[h3].p;
             p.H = spec ? (int)hl : 0;
-            p.tsa = tsa ? 1 : 0;
+            // a small call's chunks in one wave check and repair themselves (tsa 2:
+            // no flag / repair / verify launches on the call's critical path)
+            static const bool tsa_sep = LDSP_KNOB("LDSP_AGC_TSA_SEPARATE", 0) != 0;
+            p.tsa = tsa ? (p.nchunks <= 64 && !tsa_sep && !LDSP_KNOB("LDSP_DEBUG_AGC", 0) ? 2 : 1) : 0;
+            if (p.tsa == 2 && q->tsa_perturb) p.tsa |= 4;
         }
         // the next call's history first: its front then waits for this copy only
         if (n > 0) k::delay_hist(dx, q->hist[h3].p, q->hist[(h3 + 1) % 3].p, n, (int)hl, e.stream);
@@ -1865,7 +1890,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         if (n > 0) {
             if (par || tsa) {
                 if (spec) k::agc_spec_verify(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
-                else k::agc_spec_back(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
+                else if (!(p.tsa & 2)) k::agc_spec_back(dx, n, q->dst.as<k::AgcState>(), p, dy, dstat, e.stream);
                 if (dbg) {
                     unsigned c[8];
                     LDSP_HIP(hipMemcpyAsync(c, p.dbg, sizeof(c), hipMemcpyDeviceToHost, e.stream));

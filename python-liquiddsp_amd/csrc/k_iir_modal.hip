@@ -289,9 +289,14 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
     // one contiguous range of units each, so a unit's predecessors were published
     // into the same L2 (plain stores, read back with L2-served sc1 loads).  The
     // first J units of a range need units of another range: those recompute them.
+    // A small call (p.one_xcd) runs every unit on block 0's XCD instead: its
+    // ranges would be a few units long and their first units' recomputes of
+    // up to J predecessors would set the call's latency.
     const long xq = blockIdx.x & 7, xi = blockIdx.x >> 3;
+    if (p.one_xcd && xq != 0) return;
     long range0 = 0;
-    for (long y = 0; y < xq; y++) range0 += (nw - y + 7) >> 3;
+    if (!p.one_xcd)
+        for (long y = 0; y < xq; y++) range0 += (nw - y + 7) >> 3;
     const long w = range0 + xi;
     const long wb = w * kUnit;
     const bool full = wb + kUnit <= n;
@@ -447,8 +452,8 @@ void launch_modal(const IirModalCoef& cf, const void* x, size_t n, const double*
 {
     const long nw = iir_modal_units(n);
     LDSP_PROF(s, "k_iir_modal");
-    hipLaunchKernelGGL((k_iir_modal<NC, M, IQ16>), dim3((unsigned)nw), dim3(64 * NC), 0, s, cf, x, (long)n, nw, p,
-                       st_in, st_out, y);
+    hipLaunchKernelGGL((k_iir_modal<NC, M, IQ16>), dim3((unsigned)(p.one_xcd ? 8 * nw : nw)), dim3(64 * NC), 0, s, cf,
+                       x, (long)n, nw, p, st_in, st_out, y);
 }
 
 } // namespace

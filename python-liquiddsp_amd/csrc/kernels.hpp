@@ -136,6 +136,8 @@ struct IirModalPlan {
     uint64_t* agg;        // [nunits][ncomp][M * 4] {32-bit half, epoch} granules (zeroed when allocated)
     uint32_t epoch;       // per call, never 0
     int recompute = 0;    // test hook: every wave recomputes its predecessors instead of reading them
+    int one_xcd = 0;      // small call: every unit on the XCD of block 0 (a grid of 8 x units, the
+                          // blocks of the other XCDs return at once), so no unit recomputes a predecessor
     int variant = 0;      // tuning builds only (timing experiments, wrong outputs): bit 0 no look-back,
                           // bit 1 no pass 2, bit 2 no pass 1 / scan
 };
@@ -156,6 +158,8 @@ struct SpecPlan {
     const void* hist = nullptr;   // AGC: the H input samples before x[0] (H > 0: every chunk speculative)
     int H = 0;
     int tsa = 0;          // AGC small call: every chunk approximates from the true state up to its start
+                          // (2: one wave, which also checks and repairs the chunks in order;
+                          // | 4: test hook, every chunk's start state 1 ulp off)
 };
 // scratch for iir_spec: chunk states + verifier flag words
 size_t spec_flags_offset(long nchunks, int ncomp, int fs);

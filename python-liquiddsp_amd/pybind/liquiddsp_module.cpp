@@ -1151,6 +1151,13 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def_property("gain", &AGC::get_gain, &AGC::set_gain)
         .def_property("scale", &AGC::get_scale, &AGC::set_scale)
         .def_property_readonly("status", &AGC::status)
+        .def("_tsa_perturb", [](AGC& a, bool on) { check(ldsp_debug_agc_tsa_perturb(a.q, on ? 1 : 0)); },
+             "test hook: small calls re-run every chunk in-kernel (ldsp_debug_agc_tsa_perturb)")
+        .def("_tsa_reruns", [](AGC& a) {
+            unsigned c = 0;
+            check(ldsp_debug_agc_tsa_reruns(a.q, &c));
+            return c;
+        })
         .def_property(
             "onRise", [](AGC& a) { return a.mOnRise; }, [](AGC& a, py::object f) { a.mOnRise = f; })
         .def("print", &AGC::print)

@@ -148,3 +148,17 @@ def test_modal_device_tensor_streams(ld, rng):
     torch.cuda.synchronize()
     for u, v in zip(ya, yb):
         assert torch.equal(u.view(torch.int64), v.view(torch.int64))
+
+
+@pytest.mark.parametrize("n", [65_536, 200_001])
+def test_modal_small_call_one_xcd_bitwise(ld, rng, n):
+    """Small calls (up to 16 J units) run every unit on one XCD and read every
+    predecessor's published state: bit-identical to recomputing them all."""
+    x = cgauss(rng, 3 * n)
+    kw = PROTOS[0][0]
+    a, b = ld.ComplexIIRFilter(**kw), ld.ComplexIIRFilter(**kw)
+    a._scan_path(2)
+    b._scan_path(3)
+    cuts = [0, n, 2 * n, 3 * n]
+    ya, yb = _run(a, x, cuts), _run(b, x, cuts)
+    assert np.array_equal(ya.view(np.uint32), yb.view(np.uint32))

@@ -121,3 +121,37 @@ def test_agc_small_calls_low_bandwidth(ld, ora, rng):
     ys = [g(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
     rs = [o(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
     assert_bitwise(np.concatenate(ys), np.concatenate(rs))
+
+
+@pytest.mark.parametrize("squelch", [False, True])
+def test_agc_small_calls_inkernel_repair(ld, ora, rng, squelch):
+    """One-wave small calls check and repair their chunks in the chunk kernel
+    (no flag / repair / verify launches).  With every chunk's start state
+    pushed 1 ulp off (test hook) each chunk is re-run there, in order, from its
+    predecessor's end state: still bit-identical, squelch mode and timer
+    included, and so are the unperturbed calls after it."""
+    loud = _am(rng, 40_000, 48000.0, 300.0)
+    quiet = (1e-3 * (rng.standard_normal(20_000) + 1j * rng.standard_normal(20_000))).astype(np.complex64)
+    x = np.concatenate([loud, quiet, loud])
+    g = ld.AGC()
+    g.lock = False
+    g.scale = 0.01
+    o = ora.AGC()
+    o.scale = np.float32(0.01)
+    if squelch:
+        g.squelch = True
+        g.threshold = -10.0
+        o.squelch(True)
+        o.threshold = np.float32(-10.0)
+    sizes = [320, 1573, 2048, 4001, 257 * 17, 6000, 1573, 999]
+    cuts = np.concatenate([[0], np.cumsum(sizes * 20)])
+    cuts = cuts[cuts <= len(x)]
+    ys, rs = [], []
+    for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        g._tsa_perturb(i < 2 * len(sizes))
+        ys.append(g(x[a:b]))
+        rs.append(o(x[a:b]))
+    assert_bitwise(np.concatenate(ys), np.concatenate(rs))
+    assert np.float32(g.gain) == np.float32(o.gain)
+    if squelch:
+        assert g.status == o.status
