@@ -124,8 +124,8 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
 // sample and the table index only, so wave 0 evaluates them for the next batch
 // of kSqBatch samples at kSqCand indices each (around the trajectory
 // extrapolated with the last kicks held) beside the current batch's steps, and
-// a step is an index lookup plus two adds.  A batch whose index leaves its
-// window is redone with pll_eval.  Same bits as k_pll_seq.
+// a step is an index lookup plus two adds.  A step whose index leaves its
+// window is evaluated with pll_eval.  Same bits as k_pll_seq.
 constexpr int kSqBatch = 4;
 constexpr int kSqCand = 16;
 
@@ -188,36 +188,33 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
                 const int i0 = b * kSqBatch;
                 const SqCand nx = sq_cands(b0, b1, i0 + kSqBatch, cnt, tab, theta, d, k1h, k2h, alpha, beta,
                                            in.mod_index, kSqBatch, lane);
-                const uint32_t th0 = theta, d0 = d, k1s = k1h, k2s = k2h;
+                // A sample whose index left its window is evaluated directly and the
+                // batch goes on from the state it gives (scripts/analysis/pll_predict.py:
+                // a third of the batches miss at horizons 4..7 on the bench signal, mostly
+                // in their last samples, so re-running whole batches cost ~4x the misses).
                 bool miss = false;
 #pragma unroll
                 for (int j = 0; j < kSqBatch; j++) {
                     const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)cc.base, j * kSqCand);
                     const uint32_t off = (tidx(theta) - bj) & 0x3ffu;
-                    miss |= off >= (uint32_t)kSqCand;
-                    const int ln = __builtin_amdgcn_readfirstlane(j * kSqCand + (int)(off & (kSqCand - 1)));
-                    k1h = (uint32_t)__builtin_amdgcn_readlane((int)cc.k1, ln);
-                    k2h = (uint32_t)__builtin_amdgcn_readlane((int)cc.k2, ln);
-                    const float o = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.out), ln));
+                    float o;
+                    if (off < (uint32_t)kSqCand) {
+                        const int ln = __builtin_amdgcn_readfirstlane(j * kSqCand + (int)off);
+                        k1h = (uint32_t)__builtin_amdgcn_readlane((int)cc.k1, ln);
+                        k2h = (uint32_t)__builtin_amdgcn_readlane((int)cc.k2, ln);
+                        o = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.out), ln));
+                    } else {
+                        miss = true;
+                        const Kick k = pll_eval(tab, tidx(theta), b0[i0 + j], b1[i0 + j], alpha, beta, in.mod_index, 0);
+                        k1h = k.k1;
+                        k2h = k.k2;
+                        o = k.out;
+                    }
                     d += k1h;
                     theta += k2h + d;
                     ob[(i0 + j) * (lane == 0) + ooff] = o;
                 }
-                if (miss) {      // an index left its window: redo the batch directly
-                    theta = th0;
-                    d = d0;
-                    k1h = k1s;
-                    k2h = k2s;
-                    nredo++;
-                    for (int j = 0; j < kSqBatch; j++) {
-                        const Kick k = pll_eval(tab, tidx(theta), b0[i0 + j], b1[i0 + j], alpha, beta, in.mod_index, 0);
-                        d += k.k1;
-                        theta += k.k2 + d;
-                        k1h = k.k1;
-                        k2h = k.k2;
-                        ob[(i0 + j) * (lane == 0) + ooff] = k.out;
-                    }
-                }
+                nredo += miss ? 1u : 0u;
                 cc = nx;
             }
             for (int i = nb * kSqBatch; i < cnt; i++) {

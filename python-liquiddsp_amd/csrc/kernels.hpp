@@ -205,7 +205,7 @@ struct AmpState {         // device-resident PLL state
     float alpha, beta;
     uint32_t gth[2], gd[2];   // ping-pong guess of the state at the next call's start (candidate end state)
     uint32_t sq_batches;      // k_pll_seqc diagnostics, cumulative: candidate batches stepped,
-    uint32_t sq_redone;       //   and batches redone with pll_eval (an index left its window)
+    uint32_t sq_redone;       //   and batches with a step evaluated by pll_eval (an index left its window)
 };
 // One AmpModem / BroadcastAM PLL call.  x0 = lowpass(x) (precomputed), x1 =
 // delay_m(x) via hist (m samples before x[0]); writes Re(v1)/mod (carrier) or
