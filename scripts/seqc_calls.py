@@ -1,6 +1,5 @@
-"""AmpModem short-call loop (k_pll_seqh, helper-wave candidates) on the README
-chain: per-call kernel time and batches redone for the horizon D of the tuning
-build's LDSP_PLL_SEQH_D (0 = the one-wave k_pll_seqc).  One JSON line."""
+"""AmpModem short-call loop (k_pll_seqc) on the README chain's AmpModem input:
+per-call kernel time and the batches with a directly evaluated step.  One JSON line."""
 import json
 import os
 import sys
@@ -32,6 +31,6 @@ torch.cuda.synchronize()
 L._profile_enable(False)
 b1, r1 = am._seq_stats()
 rep = {k: round(v[1] / v[0] * 1e3, 1) for k, v in L._profile_report().items()}
-print(json.dumps({"D": os.environ.get("LDSP_PLL_SEQH_D", "default"), "samples_per_call": int(ins[0].numel()),
+print(json.dumps({"samples_per_call": int(ins[0].numel()),
                   "kernel_us": rep, "batches": b1 - b0, "redone": r1 - r0,
                   "redone_frac": round((r1 - r0) / max(1, b1 - b0), 4)}))
