@@ -180,7 +180,11 @@ int ldsp_nco_mix_firfilt(ldsp_nco_t nco, ldsp_firfilt_t fir, const void *x, size
  * accurate than liquid's float32 recursion): in one pass over memory in the
  * filter's modal coordinates when they are well-conditioned, else as a blocked
  * scan of the SOS state; EXACT runs the float32 direct-form II recursion
- * sequentially (bit-identical to the restatement).
+ * (bit-identical to the restatement): sequentially, or -- for filters that
+ * forget their state within 16 384 samples (de-emphasis, DC blockers) -- as
+ * speculative chunks started early from zero whose start states a verifier
+ * checks bit for bit against their predecessors' (the same bits).  Fast mode
+ * takes that path for those filters too.
  * ---------------------------------------------------------------------- */
 typedef struct ldsp_iirfilt_s *ldsp_iirfilt_t;
 int ldsp_iirfilt_create_prototype(int ftype, int btype, unsigned int order, float fc, float f0,

@@ -1606,8 +1606,11 @@ static int iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, i
         if (n > 0) {
             const k::IirDesc d = q->desc();
             enum { kSpec, kSeq, kModal, kBlk, kScan } path;
-            if (q->mode == LDSP_MODE_EXACT || q->D == 0) path = kSeq;
-            else if (q->path_force == 0 && q->spec_W > 0 && q->spec_W <= 16384) path = kSpec;   // fast-decaying: exact chunks
+            // fast-decaying filters: speculative exact chunks (the sequential
+            // loop's bits, so exact mode takes them too: FMStereo's de-emphasis)
+            if (q->D == 0) path = kSeq;
+            else if (q->path_force == 0 && q->spec_W > 0 && q->spec_W <= 16384) path = kSpec;
+            else if (q->mode == LDSP_MODE_EXACT) path = kSeq;
             else if (q->mf.ok && q->path_force != 1) path = kModal;
             else if (q->D <= k::kIirBlkMaxD) path = kBlk;
             else path = kScan;
