@@ -502,7 +502,7 @@ __device__ __forceinline__ void mix_interior(float2 (&v)[PPL], long g0, int lane
     for (int r = 0; r < PPL; r++) v[r] = nco_apply(v[r], sc[r], mx);
 }
 
-template <bool MIX, bool PREF, int WAVES>
+template <bool MIX, bool PREF, int WAVES, bool ILV = false>
 __global__ void __launch_bounds__(64 * WAVES) k_fir_fft1024x(const float2* __restrict__ x,
                                                           const float2* __restrict__ hist,
                                                           float2* __restrict__ hist_out, long n, int L, int P,
@@ -538,20 +538,25 @@ __global__ void __launch_bounds__(64 * WAVES) k_fir_fft1024x(const float2* __res
     }
     __syncthreads();
     if (blockIdx.x == 0) write_hist<MIX>(x, hist, hist_out, n, halo, t, 64 * WAVES, mx, ntab);
-    const long w0 = ((long)blockIdx.x * WAVES + wave) * per;
-    const long w1 = min(nwin, w0 + per);
+    // ILV: the workgroup's windows interleaved over its waves (wave k takes
+    // k, k + WAVES, ..), so the P-sample overlap a window shares with the next
+    // is read by another wave at about the same time, from L2, instead of by
+    // the same wave one window (~10 us) later, when it has often left L2
+    const long wb = ILV ? (long)blockIdx.x * WAVES * per + wave : ((long)blockIdx.x * WAVES + wave) * per;
+    const long we = ILV ? min(nwin, (long)(blockIdx.x + 1) * WAVES * per) : min(nwin, wb + per);
+    const long step = ILV ? WAVES : 1;
     float2* d = buf[wave];
     const float2* Hl = lH + lane;
     float2 nx[16];
-    if (PREF && w0 < w1) load_win<16>(nx, x, hist, n, halo, w0 * M - P, lane);
-    for (long w = w0; w < w1; w++) {
+    if (PREF && wb < we) load_win<16>(nx, x, hist, n, halo, wb * M - P, lane);
+    for (long w = wb; w < we; w += step) {
         const long g0 = w * M - P;
         const bool interior = g0 >= 0 && g0 + kWN_ <= n;
         float2 v[16];
         if (PREF) {
 #pragma unroll
             for (int r = 0; r < 16; r++) v[r] = nx[r];
-            if (w + 1 < w1) load_win<16>(nx, x, hist, n, halo, g0 + M, lane);
+            if (w + step < we) load_win<16>(nx, x, hist, n, halo, g0 + step * M, lane);
         } else {
             load_win<16>(v, x, hist, n, halo, g0, lane);
         }
@@ -622,7 +627,7 @@ __device__ __forceinline__ void fft512x(float2 (&v)[8], float2* d, const float2*
     dft8(v);
 }
 
-template <bool MIX>
+template <bool MIX, bool ILV = false>
 __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512x(const float2* __restrict__ x,
                                                               const float2* __restrict__ hist,
                                                               float2* __restrict__ hist_out, long n, int L, int P,
@@ -646,11 +651,12 @@ __global__ void __launch_bounds__(64 * kVWaves) k_fir_fft512x(const float2* __re
     for (int j = t; j < kVN; j += 64 * kVWaves) lH[j] = H[j];
     __syncthreads();
     if (blockIdx.x == 0) write_hist<MIX>(x, hist, hist_out, n, halo, t, 64 * kVWaves, mx, ntab);
-    const long w0 = ((long)blockIdx.x * kVWaves + wave) * per;
-    const long w1 = min(nwin, w0 + per);
+    const long wb = ILV ? (long)blockIdx.x * kVWaves * per + wave : ((long)blockIdx.x * kVWaves + wave) * per;
+    const long we = ILV ? min(nwin, (long)(blockIdx.x + 1) * kVWaves * per) : min(nwin, wb + per);
+    const long step = ILV ? kVWaves : 1;     // (k_fir_fft1024x)
     float2* d = buf[wave];
     const float2* Hl = lH + lane;
-    for (long w = w0; w < w1; w++) {
+    for (long w = wb; w < we; w += step) {
         const long g0 = w * M - P;
         const bool interior = g0 >= 0 && g0 + kVN <= n;
         float2 v[8];
@@ -697,7 +703,7 @@ long resident_waves(const void* fn, int threads)
 // (k_fir_fft1024x: 16, one workgroup per CU), bit 3 1024-point
 // windows for short filters too, bit 4 the padded-exchange k_fir_fft1024, bit 5
 // the padded-exchange k_fir_fft512.
-constexpr int kFftVariantDefault = 0;   // conflict-free exchanges; 512: 6 waves / SIMD, 1024: 4-wave blocks, no prefetch
+constexpr int kFftVariantDefault = 256;   // conflict-free exchanges, windows interleaved over waves; 512: 6 waves / SIMD, 1024: 4-wave blocks, no prefetch
 static int fft_variant()
 {
     static const int var = LDSP_KNOB("LDSP_FFT_VARIANT", kFftVariantDefault);
@@ -714,8 +720,8 @@ static void fft_launch(bool small, int var, unsigned grid_of_waves_fn_unused, co
 {
     (void)grid_of_waves_fn_unused;
     auto run = [&](const void* fn, int wpb, auto launch) {
-        static long slots_cache[2][512] = {};
-        long& slots = slots_cache[MIX ? 1 : 0][(small ? 256 : 0) | (var & 255)];
+        static long slots_cache[2][1024] = {};
+        long& slots = slots_cache[MIX ? 1 : 0][(small ? 512 : 0) | (var & 511)];
         if (slots == 0) slots = resident_waves(fn, 64 * wpb);
         const long waves = std::min(nwin, slots);
         const long per = (nwin + waves - 1) / waves;       // contiguous windows per wave
@@ -729,12 +735,16 @@ static void fft_launch(bool small, int var, unsigned grid_of_waves_fn_unused, co
                            mx, tab);                                                                           \
     })
     if (small && !(var & 32)) {
-        LDSP_FFT_LAUNCH((k_fir_fft512x<MIX>), kVWaves);
+        if (var & 256) LDSP_FFT_LAUNCH((k_fir_fft512x<MIX, true>), kVWaves);
+        else LDSP_FFT_LAUNCH((k_fir_fft512x<MIX, false>), kVWaves);
     } else if (small) {
         if (var & 1) LDSP_FFT_LAUNCH((k_fir_fft512<MIX, true>), kVWaves);
         else LDSP_FFT_LAUNCH((k_fir_fft512<MIX, false>), kVWaves);
     } else if (!(var & 16)) {
-        switch ((var & 2) | (var >> 6 & 3) << 2) {
+        switch ((var & 2) | (var >> 6 & 3) << 2 | (var & 256) >> 4) {
+        case 16: LDSP_FFT_LAUNCH((k_fir_fft1024x<MIX, false, 4, true>), 4); break;
+        case 18: LDSP_FFT_LAUNCH((k_fir_fft1024x<MIX, true, 4, true>), 4); break;
+        case 28: LDSP_FFT_LAUNCH((k_fir_fft1024x<MIX, false, 16, true>), 16); break;
         case 0: LDSP_FFT_LAUNCH((k_fir_fft1024x<MIX, false, 4>), 4); break;
         case 2: LDSP_FFT_LAUNCH((k_fir_fft1024x<MIX, true, 4>), 4); break;
         case 4: LDSP_FFT_LAUNCH((k_fir_fft1024x<MIX, false, 6>), 6); break;
