@@ -7,8 +7,9 @@ PLL runs the one-wave candidate-kick loop (k_pll_seqc, below 2 048 samples;
 its own tests are in test_gpu_pll_seqc.py; Costas mode runs candidates + walk
 from 1 280 samples); both must stay bit-identical to the sequential
 restatement, including the calls whose approximate trajectory left the exact
-one (re-run by k_agc_runfix / k_agc_verify), and across calls rotating over
-several streams.
+one (a one-wave call -- up to 64 chunks -- re-runs such chunks inside
+k_agc_chunks, a larger one in k_agc_runfix / k_agc_verify), and across calls
+rotating over several streams.
 """
 import numpy as np
 import pytest
