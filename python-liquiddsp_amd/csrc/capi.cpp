@@ -120,13 +120,59 @@ static void zero_now(void* p, int v, size_t bytes)
 }
 
 // Host <-> device staging for LDSP_MEM_HOST calls
+// Host buffers pass through a pinned staging buffer (a copy from / to pageable
+// memory is staged by the runtime at a fraction of the DMA rate, and it is the
+// per-call overhead of the README's numpy callbacks); each host call ends with a
+// stream synchronize, so the next call may reuse the buffer.  Above kPinMax the
+// pageable copy is used directly (no pinned memory of that size per object).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    void* ensure(size_t bytes) {
+        if (bytes <= cap && p) return p;
+        const size_t want = (std::max(bytes, cap + cap / 4) + 65535) & ~(size_t)65535;
+        if (p) LDSP_HIP(hipHostFree(p));
+        p = nullptr;
+        cap = 0;
+        LDSP_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+        cap = want;
+        return p;
+    }
+};
 struct Staging {
+    static constexpr size_t kPinMax = (size_t)16 << 20;
     DevBuf in, out;
+    PinnedBuf hin, hout;
+    hipEvent_t hin_done = nullptr;    // the last copy out of hin (a call that threw may not have synchronized)
+    Staging() = default;
+    Staging(const Staging&) = delete;
+    Staging& operator=(const Staging&) = delete;
+    ~Staging() {
+        if (hin_done) (void)hipEventDestroy(hin_done);
+    }
+    hipEvent_t done()
+    {
+        if (!hin_done) LDSP_HIP(hipEventCreateWithFlags(&hin_done, hipEventDisableTiming));
+        return hin_done;
+    }
     const void* dev_in(const Exec& e, const void* x, size_t bytes)
     {
         if (!e.host) return x;
         in.ensure(bytes, e.device);
-        if (bytes) LDSP_HIP(hipMemcpyAsync(in.p, x, bytes, hipMemcpyHostToDevice, e.stream));
+        if (bytes && bytes <= kPinMax) {
+            LDSP_HIP(hipEventSynchronize(done()));
+            std::memcpy(hin.ensure(bytes), x, bytes);
+            LDSP_HIP(hipMemcpyAsync(in.p, hin.p, bytes, hipMemcpyHostToDevice, e.stream));
+            LDSP_HIP(hipEventRecord(hin_done, e.stream));
+        } else if (bytes) {
+            LDSP_HIP(hipMemcpyAsync(in.p, x, bytes, hipMemcpyHostToDevice, e.stream));
+        }
         return in.p;
     }
     void* dev_out(const Exec& e, void* y, size_t bytes)
@@ -137,6 +183,15 @@ struct Staging {
     void finish(const Exec& e, void* y, size_t bytes)
     {
         if (!e.host) return;
+        if (bytes && bytes <= kPinMax) {
+            LDSP_HIP(hipMemcpyAsync(hout.ensure(bytes), out.p, bytes, hipMemcpyDeviceToHost, e.stream));
+            // wait on an event (the host spins on it) rather than the stream, whose
+            // synchronize may yield the thread: a README block makes five of these waits
+            LDSP_HIP(hipEventRecord(done(), e.stream));
+            LDSP_HIP(hipEventSynchronize(hin_done));
+            std::memcpy(y, hout.p, bytes);
+            return;
+        }
         if (bytes) LDSP_HIP(hipMemcpyAsync(y, out.p, bytes, hipMemcpyDeviceToHost, e.stream));
         LDSP_HIP(hipStreamSynchronize(e.stream));
     }
