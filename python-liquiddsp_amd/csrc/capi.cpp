@@ -1180,6 +1180,7 @@ static void fir_dispatch(ldsp_firfilt_s* q, const void* dx, size_t n, void* dy, 
 
 int ldsp_firfilt_execute(ldsp_firfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_firfilt_execute");
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "firfilt_execute: NULL buffer");
@@ -1295,6 +1296,7 @@ int ldsp_resamp_num_outputs(ldsp_resamp_t q, size_t n, size_t* nout)
 int ldsp_resamp_execute(ldsp_resamp_t q, const void* x, size_t n, void* y, size_t cap, size_t* nout, int mem,
                         void* stream)
 {
+    LDSP_RANGE("ldsp_resamp_execute");
     return guard([&] {
         NONNULL(q);
         const size_t K = q->num_outputs(n);
@@ -1411,6 +1413,7 @@ int ldsp_nco_set_state(ldsp_nco_t q, uint32_t t, uint32_t d)
 
 int ldsp_nco_mix(ldsp_nco_t q, const void* x, size_t n, void* y, int down, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_nco_mix");
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "nco_mix: NULL buffer");
@@ -1430,6 +1433,7 @@ int ldsp_nco_mix(ldsp_nco_t q, const void* x, size_t n, void* y, int down, int m
 int ldsp_nco_mix_firfilt(ldsp_nco_t nco, ldsp_firfilt_t q, const void* x, size_t n, void* y, int down, int mem,
                          void* stream)
 {
+    LDSP_RANGE("ldsp_nco_mix_firfilt");
     return guard([&] {
         NONNULL(nco);
         NONNULL(q);
@@ -1721,10 +1725,12 @@ static int iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, i
 }
 int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_iirfilt_execute");
     return iirfilt_execute(q, x, n, y, mem, stream, false);
 }
 int ldsp_iirfilt_execute_iq16(ldsp_iirfilt_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_iirfilt_execute_iq16");
     return iirfilt_execute(q, x, n, y, mem, stream, true);
 }
 
@@ -1861,6 +1867,7 @@ int ldsp_agc_set_mode(ldsp_agc_t q, int mode)
 // checks chunk 0 against the true state, repairs and verifies, and advances it.
 int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* status, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_agc_execute");
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "agc_execute: NULL buffer");
@@ -2145,6 +2152,7 @@ static void amp_call_end(AmpObj* q, const Exec& e)
 
 int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_ampmodem_demodulate");
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "ampmodem_demodulate: NULL buffer");
@@ -2228,6 +2236,7 @@ int ldsp_bcastam_get_mode(ldsp_bcastam_t q, int* mode)
 }
 int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void* x, size_t n, void* y, void* pre, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_bcastam_demodulate");
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "bcastam_demodulate: NULL buffer");
@@ -2291,6 +2300,7 @@ int ldsp_freqdem_get_kf(ldsp_freqdem_t q, float* kf)
 }
 int ldsp_freqdem_demodulate(ldsp_freqdem_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_freqdem_demodulate");
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "freqdem_demodulate: NULL buffer");
@@ -2355,6 +2365,7 @@ int ldsp_delay_get_delay(ldsp_delay_t q, unsigned int* nd)
 }
 int ldsp_delay_execute(ldsp_delay_t q, const void* x, size_t n, int cplx, void* y, int mem, void* stream)
 {
+    LDSP_RANGE("ldsp_delay_execute");
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "delay_execute: NULL buffer");
@@ -2470,6 +2481,7 @@ int ldsp_fmstereo_get_state(ldsp_fmstereo_t q, uint32_t* theta, uint32_t* dtheta
 int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, size_t cap, size_t* nout, int mem,
                           void* stream)
 {
+    LDSP_RANGE("ldsp_fmstereo_execute");
     return guard([&] {
         NONNULL(q);
         size_t k = 0;

@@ -10,6 +10,7 @@
 #include <string>
 
 #include "../../include/ldsp.h"
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 namespace ldsp {
 
@@ -45,6 +46,16 @@ struct Scope {
 #define LDSP_PROF_CAT2(a, b) a##b
 #define LDSP_PROF_CAT(a, b) LDSP_PROF_CAT2(a, b)
 #define LDSP_PROF(stream, name) ::ldsp::prof::Scope LDSP_PROF_CAT(ldsp_prof_, __LINE__)((stream), (name))
+
+// roctx range around a C-ABI call (SURVEY section 5 tracing): visible in
+// `rocprofv3 --marker-trace`, a table lookup otherwise.
+struct RoctxRange {
+    explicit RoctxRange(const char* m) { roctxRangePushA(m); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange&) = delete;
+    RoctxRange& operator=(const RoctxRange&) = delete;
+};
+#define LDSP_RANGE(name) ::ldsp::RoctxRange LDSP_PROF_CAT(ldsp_range_, __LINE__)(name)
 
 #define LDSP_REQUIRE(cond, msg)                                                            \
     do {                                                                                   \
