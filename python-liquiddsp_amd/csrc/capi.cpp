@@ -1924,9 +1924,15 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             // bandwidth 0.01) for its C outputs, so C = 1024 does a quarter of the
             // front's work of C = 256 at ~20 % more latency (hidden under the PLL
             // walk in a streamed chain); measured on 8 channels per GPU 6.6 -> 6.3
-            // ms per step (scripts/agc_chunk_sweep.sh).  Small calls (tsa) keep 256.
+            // ms per step (scripts/agc_chunk_sweep.sh).  Small calls (tsa): the
+            // one wave runs the approximate loop up to the last chunk's start and
+            // then C exact steps, so the shortest chunks that still fit 64 lanes
+            // (C >= 32) cut the exact tail: a README call (1 573 samples) 256 -> 32
+            // exact steps after the same approximate run.  Multi-wave tsa calls keep 256.
             static const int agc_c = LDSP_KNOB("LDSP_AGC_C", 1024);
-            p.C = tsa ? 256 : agc_c;
+            static const int tsa_cmin = LDSP_KNOB("LDSP_AGC_TSA_CMIN", 32);
+            const int c64 = (int)(((n + 63) / 64 + 31) / 32 * 32);      // 64 chunks of a multiple of 32
+            p.C = tsa ? (c64 <= 256 ? std::max(tsa_cmin, c64) : 256) : agc_c;
             p.nchunks = (long)((n + p.C - 1) / p.C);
             p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks), q->device);
             p.hist = q->hist[h3].p;
