@@ -1667,8 +1667,9 @@ static int iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, i
             enum { kSpec, kSeq, kModal, kBlk, kScan } path;
             // fast-decaying filters: speculative exact chunks (the sequential
             // loop's bits, so exact mode takes them too: FMStereo's de-emphasis)
+            static const long spec_min = LDSP_KNOB("LDSP_IIR_SPEC_MIN", 0L);
             if (q->D == 0) path = kSeq;
-            else if (q->path_force == 0 && q->spec_W > 0 && q->spec_W <= 16384) path = kSpec;
+            else if (q->path_force == 0 && q->spec_W > 0 && q->spec_W <= 16384 && (long)n >= spec_min) path = kSpec;
             else if (q->mode == LDSP_MODE_EXACT) path = kSeq;
             else if (q->mf.ok && q->path_force != 1) path = kModal;
             else if (q->D <= k::kIirBlkMaxD) path = kBlk;

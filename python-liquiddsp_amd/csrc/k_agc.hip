@@ -347,6 +347,60 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
     gs[7] = r.timer;
 }
 
+// One-wave small call (tsa 2) with the call's input staged in LDS first: the
+// approximate loop of every lane runs up to its chunk's start over the same
+// prefix of x, and from global memory each batch of loads costs an L2 / HBM
+// round trip on the dependent chain (~0.13 us a step); from LDS the loop is
+// compute-bound.  Otherwise the tsa 2 path of k_agc_chunks.
+constexpr long kAgcSmallMax = 8192;      // samples staged (64 KB of LDS)
+__global__ void __launch_bounds__(64) k_agc_small(const float2* __restrict__ x, long n, AgcState* st, int C, long nch,
+                                                  float2* __restrict__ y, uint8_t* __restrict__ status, int perturb)
+{
+    LDSP_LATENCY_CRITICAL();
+    extern __shared__ float2 xs[];
+    const int lane = threadIdx.x;
+    for (long i = lane; i < n; i += 64) xs[i] = x[i];
+    __syncthreads();
+    const long chunk = lane;
+    if (chunk >= nch) return;
+    const AgcState p = *st;
+    const float2* xl = xs;
+    const long s0 = chunk * C, s1 = min(n, s0 + C);
+    AgcReg r{p.g, p.y2p, p.mode, p.timer};
+    agc_run_approx(r, p, xl, 0, s0);
+    if (perturb && chunk > 0) r.g = __uint_as_float(__float_as_uint(r.g) + 1u);   // test hook
+    const AgcReg s = r;
+    agc_run<true>(r, p, xl, s0, s1, y, status);
+    auto differs = [&](const AgcReg& e_prev) {
+        return __float_as_uint(s.g) != __float_as_uint(e_prev.g) || __float_as_uint(s.y2p) != __float_as_uint(e_prev.y2p) ||
+               s.mode != e_prev.mode || s.timer != e_prev.timer;
+    };
+    auto up = [&](const AgcReg& e) {
+        return AgcReg{__shfl_up(e.g, 1), __shfl_up(e.y2p, 1), __shfl_up(e.mode, 1), __shfl_up(e.timer, 1)};
+    };
+    AgcReg pe = up(r);
+    uint64_t bad = __ballot(lane >= 1 && differs(pe));
+    int reruns = 0;
+    while (bad) {
+        reruns++;
+        const int j = __builtin_ctzll(bad);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        AgcReg e{__shfl(r.g, j - 1), __shfl(r.y2p, j - 1), __shfl(r.mode, j - 1), __shfl(r.timer, j - 1)};
+        if (lane == 0) agc_run<true>(e, p, xl, (long)j * C, min(n, (long)j * C + C), y, status);
+        const AgcReg f{__shfl(e.g, 0), __shfl(e.y2p, 0), __shfl(e.mode, 0), __shfl(e.timer, 0)};
+        if (lane == j) r = f;
+        pe = up(r);
+        bad = __ballot(lane > j && differs(pe));
+    }
+    if (lane == (int)(nch - 1)) {
+        st->g = r.g;
+        st->y2p = r.y2p;
+        st->mode = r.mode;
+        st->timer = r.timer;
+        if (reruns) st->pad[0] += reruns;     // ldsp_debug_agc_tsa_reruns
+    }
+}
+
 // Parallel repair round over runs of failed chunks.  flags (k_agc_flags)
 // mark the chunks whose guessed start state differs from the predecessor's
 // end state; one thread per run start (flagged chunk with an unflagged
@@ -533,6 +587,13 @@ size_t agc_scratch_bytes(long nchunks) { return (agc_flags_offset_words(nchunks)
 void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
+    if ((p.tsa & 2) && p.nchunks <= 64 && (long)n <= kAgcSmallMax) {
+        LDSP_PROF(s, "k_agc_chunks");
+        hipLaunchKernelGGL(k_agc_small, dim3(1), dim3(64), n * sizeof(float2), s, (const float2*)x, (long)n, st, p.C,
+                           p.nchunks, (float2*)y, status, (p.tsa & 4) ? 1 : 0);
+        LDSP_HIP(hipGetLastError());
+        return;
+    }
     {
         LDSP_PROF(s, "k_agc_chunks");
         hipLaunchKernelGGL(k_agc_chunks, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, (const float2*)x,

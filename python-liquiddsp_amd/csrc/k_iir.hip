@@ -190,13 +190,26 @@ __device__ __forceinline__ void run_f32(StepF&& step, const float* __restrict__ 
 
 // --------------------------------------------------------------- speculative exact
 // scratch layout: [nchunks][2 (guess, end)][ncomp][fstate]  + flags
-template <int Z>
-__global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* __restrict__ x, long n, int ncomp,
+// STAGE: the workgroup first copies its chunks' input window (64 chunk-lanes x C
+// samples + W of warm-up) into LDS with coalesced loads; the lanes' loops then
+// read LDS.  From global memory each batch of 8 steps waited an L2 / HBM round
+// trip (~150 ns a step for a first-order filter, whose step is ~10 ns).
+template <int Z, bool STAGE>
+__global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* __restrict__ xg, long n, int ncomp,
                                                         const float* __restrict__ state0, int C, int W, long nch,
                                                         float* __restrict__ sc, float* __restrict__ y)
 {
     LDSP_LATENCY_CRITICAL();
+    extern __shared__ float xs[];
     const long ch = (long)blockIdx.x * 64 + threadIdx.x;
+    const float* x = xg;
+    if (STAGE) {
+        const long first = (long)blockIdx.x * 64 / ncomp, last = min(nch - 1, ((long)blockIdx.x * 64 + 63) / ncomp);
+        const long lo = max(0L, first * C - W), hi = min(n, (last + 1) * C);
+        for (long i = threadIdx.x; i < (hi - lo) * ncomp; i += 64) xs[i] = xg[lo * ncomp + i];
+        __syncthreads();
+        x = xs - lo * ncomp;            // x[i * ncomp + c] for lo <= i < hi
+    }
     if (ch >= nch * ncomp) return;
     const long chunk = ch / ncomp;
     const int c = (int)(ch % ncomp);
@@ -946,13 +959,23 @@ void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state
     const int z = iir_size_class(d);
     {
         LDSP_PROF(s, "k_iir_spec_chunks");
+        // a workgroup's window: 64 / ncomp chunks of C samples + W, ncomp floats each
+        const size_t stage = (size_t)4 * (64 * (size_t)p.C + (size_t)ncomp * p.W);
+        const bool st = stage <= 64 * 1024;
         auto launch = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned)((work + 63) / 64)), dim3(64), 0, s, d, (const float*)x, (long)n,
-                               ncomp, (const float*)state, p.C, p.W, p.nchunks, (float*)p.scratch, (float*)y);
+            hipLaunchKernelGGL(kern, dim3((unsigned)((work + 63) / 64)), dim3(64), st ? stage : 0, s, d,
+                               (const float*)x, (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks,
+                               (float*)p.scratch, (float*)y);
         };
-        if (z == 2) launch(k_iir_spec_chunks<2>);
-        else if (z == 4) launch(k_iir_spec_chunks<4>);
-        else launch(k_iir_spec_chunks<kMaxTf>);
+        if (st) {
+            if (z == 2) launch(k_iir_spec_chunks<2, true>);
+            else if (z == 4) launch(k_iir_spec_chunks<4, true>);
+            else launch(k_iir_spec_chunks<kMaxTf, true>);
+        } else {
+            if (z == 2) launch(k_iir_spec_chunks<2, false>);
+            else if (z == 4) launch(k_iir_spec_chunks<4, false>);
+            else launch(k_iir_spec_chunks<kMaxTf, false>);
+        }
     }
     LDSP_HIP(hipGetLastError());
     const int fs = d.sos ? 3 * d.nsos : d.nv;
