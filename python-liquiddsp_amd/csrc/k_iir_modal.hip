@@ -335,14 +335,6 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
             g[4 * k + 3] = tag | (uint32_t)(bi >> 32);
         }
     }
-    // this lane's exclusive prefix E_{t-1}
-    Modal<M> z;
-#pragma unroll
-    for (int k = 0; k < M; k++) {
-        const double er = __shfl_up(E.w0[k], 1), ei = __shfl_up(E.w1[k], 1);
-        z.w0[k] = lane == 0 ? 0.0 : er;
-        z.w1[k] = lane == 0 ? 0.0 : ei;
-    }
 
     // look-back: lane i < jw fetches BL_{w-1-i} (S_call when i == w)
 #ifdef LDSP_TUNING
@@ -409,6 +401,17 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
             }
         }
         comp_load<NC, IQ16>(xv, n, w, lane, c, pl[c]);
+#pragma unroll
+        for (int s = 0; s < kC; s++) u[s] = row[s];
+        modal_scan<M>(cf, p.PS, u, lane, E);
+    }
+    // this lane's exclusive prefix E_{t-1}
+    Modal<M> z;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+        const double er = __shfl_up(E.w0[k], 1), ei = __shfl_up(E.w1[k], 1);
+        z.w0[k] = lane == 0 ? 0.0 : er;
+        z.w1[k] = lane == 0 ? 0.0 : ei;
     }
     // S_w = sum_i A^(2048 i) a_i, in order of i, on wave-uniform values (the
     // predecessors' states read lane by lane, the powers as scalar loads);

@@ -1,9 +1,10 @@
 """Fast-mode ComplexIIRFilter at 64 Mi samples (the chain's first stage, cheby2
 order 8): the modal single-pass scan against the blocked scan, complex64 and
-int16 IQ (from_bytes) input; per-kernel device times from libldsp's HIP events."""
+int16 IQ (from_bytes) input; per-kernel device times from libldsp's HIP events.
+LDSP_PKG_DIR selects another build of the package (A/B runs)."""
 import json, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [REPO, os.path.join(REPO, "python-liquiddsp_amd")]
+sys.path[:0] = [REPO, os.environ.get("LDSP_PKG_DIR") or os.path.join(REPO, "python-liquiddsp_amd")]
 import torch
 import liquiddsp as L
 
