@@ -1,9 +1,9 @@
 #!/bin/bash
 # A/B timing of the IIR kernels: scripts/iir_bench.py on a saved build of the
 # package (OLD, default build_ab: libldsp.so + liquiddsp/ copied before a
-# change) and on the tree's build under each LDSP_IIR_PERSIST setting in
-# PERSIST (default: the library's own choice only) and on the saved builds in
-# VARIANTS, alternated twice; then the
+# change), on the saved builds in VARIANTS and on the tree's build, alternated
+# twice (PERSIST: LDSP_IIR_PERSIST settings, read by tuning builds only -- the
+# knob of the persistent experiment in DESIGN.md section 4, since removed); then the
 # modal GPU tests.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 OLD=${OLD:-build_ab}
