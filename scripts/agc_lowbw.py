@@ -3,7 +3,8 @@ samples, so every shorter call runs tsa mode (chunks approximating from the
 call's true start state).  Times each call size, counts in-kernel / runfix
 re-runs and checks every call bitwise against the restatement.  Run once as is
 and once with LDSP_AGC_TSAMIN=1000000000 (tsa off: those calls take the
-sequential / speculative path) to compare."""
+sequential / speculative path) to compare -- the LDSP_* knobs are read only by
+a tuning build (Makefile EXTRA=-DLDSP_TUNING; LDSP_PKG_DIR points at it)."""
 import json
 import os
 import sys
@@ -12,7 +13,7 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [REPO, os.path.join(REPO, "python-liquiddsp_amd")]
+sys.path[:0] = [REPO, os.environ.get("LDSP_PKG_DIR") or os.path.join(REPO, "python-liquiddsp_amd")]
 import torch  # noqa: E402
 import liquiddsp as L  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (checker only)
