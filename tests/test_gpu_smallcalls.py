@@ -105,20 +105,23 @@ def test_amradio_readme_blocks_rotating_streams(ld, ora):
     assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), np.concatenate(refs))
 
 
-def test_agc_small_calls_low_bandwidth(ld, ora, rng):
-    """At bandwidth 1e-3 the chunk-parallel threshold grows to ~62 k samples, so
-    calls up to that length run tsa mode: every chunk approximates from the true
-    state over up to ~60 k samples.  Calls at the top of that range stay
-    bit-identical (a trajectory that leaves the exact one is re-run)."""
-    x = _am(rng, 200_000, 48000.0, 300.0)
+@pytest.mark.parametrize("bw", [1e-3, 1e-4])
+def test_agc_small_calls_low_bandwidth(ld, ora, rng, bw):
+    """At bandwidth 1e-3 (1e-4) the chunk-parallel threshold grows to ~62 k
+    (~617 k) samples, so calls up to that length run tsa mode: every chunk
+    approximates from the true state over up to that many samples.  Calls at the
+    top of that range stay bit-identical (a trajectory that leaves the exact one
+    is re-run); scripts/agc_lowbw.py times them."""
+    s = 10 if bw < 5e-4 else 1
+    x = _am(rng, 200_000 * s, 48000.0, 300.0)
     g = ld.AGC()
-    g.bandwidth = 1e-3
+    g.bandwidth = bw
     g.lock = False
     g.scale = 0.01
     o = ora.AGC()
-    o.bandwidth = np.float32(1e-3)
+    o.bandwidth = np.float32(bw)
     o.scale = np.float32(0.01)
-    cuts = [0, 10_000, 70_000, 130_000, 190_000, 200_000]
+    cuts = [c * s for c in (0, 10_000, 70_000, 130_000, 190_000, 200_000)]
     ys = [g(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
     rs = [o(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
     assert_bitwise(np.concatenate(ys), np.concatenate(rs))
