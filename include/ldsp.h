@@ -262,13 +262,21 @@ int ldsp_agc_execute(ldsp_agc_t q, const void *x, size_t n, void *y, uint8_t *st
 /* ------------------------------------------------------------------------
  * AM demodulator: ampmodem (type 0 dsb, 1 usb, 2 lsb).  Replaces AmpModem
  * (src/demod.hpp:221-307: ampmodem_create(mod, type, suppressed_carrier),
- * ampmodem_demodulate_block, ampmodem_reset).
+ * ampmodem_demodulate_block, ampmodem_reset).  dsb: carrier PLL (carrier) or
+ * Costas loop (suppressed); usb / lsb: the carrier PLL then a Hilbert c2r
+ * (carrier), or the Hilbert c2r alone (suppressed).
  * ---------------------------------------------------------------------- */
 typedef struct ldsp_ampmodem_s *ldsp_ampmodem_t;
 int ldsp_ampmodem_create(float mod_index, int type, int suppressed_carrier, ldsp_ampmodem_t *q);
 int ldsp_ampmodem_destroy(ldsp_ampmodem_t q);
 int ldsp_ampmodem_reset(ldsp_ampmodem_t q);
 int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t *theta, uint32_t *dtheta);
+/* The designs inside (liquid ampmodem_create): carrier lowpass (2m+1 = 51 taps,
+ * firfilt_crcf_create_kaiser(51, 0.01, 40, 0)), DC blocker (51 taps,
+ * firfilt_rrrf_create_dc_blocker(25, 20)) and the usb / lsb Hilbert transform's
+ * 2m = 50 quadrature taps (firhilbf_create(25, 60), see firhilb.proto.c).  Any
+ * pointer may be NULL.  Host only. */
+int ldsp_ampmodem_get_taps(ldsp_ampmodem_t q, float *lowpass, float *dcblock, float *hilbert);
 int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void *x, size_t n, void *y, int mem,
                              void *stream);
 /* Diagnostics, no reference counterpart: the exact PLL walk of the last call

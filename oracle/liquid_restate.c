@@ -1514,8 +1514,87 @@ void ora_agc_execute_wrapper(ora_agc q, const float *x, size_t n, float *y, uint
 }
 
 /* ===================================================================== */
+/* firhilbf (complex -> real): liquid src/filter/src/firhilb.proto.c      */
+/* (liquid >= 1.4, as recalled; parity unpinned)                          */
+/*   h = firdes_kaiser(4m+1, 0.25, As, 0);  h[i] = imag(h[i] e^{j pi t/2}) */
+/*   with t = i - 2m (non-zero at odd t only: a unit-gain Hilbert          */
+/*   transformer, the half-band prototype's passband gain being 2);        */
+/*   hq[j] = h[4m - 1 - 2j], j < 2m (the odd taps, reversed).  liquid runs */
+/*   c2r on polyphase windows (even / odd samples, toggled per call); in    */
+/*   full-rate terms every output is                                        */
+/*     yi = re x[n - 2m],  yq = sum_j hq[j] im x[n - 4m + 1 + 2j]           */
+/*     (dotprod order, oldest first),  y0 = yi + yq (LSB),  y1 = yi - yq    */
+/*   (USB), with zero history after create / reset.                          */
+/* ===================================================================== */
+struct ora_firhilb_s {
+    unsigned int m;
+    float *hq;                 /* 2m quadrature taps */
+    ora_window w;              /* last 4m complex inputs */
+};
+typedef struct ora_firhilb_s *ora_firhilb;
+
+ora_firhilb ora_firhilb_create(unsigned int m, float as)
+{
+    if (m < 2) return NULL;
+    ora_firhilb q = (ora_firhilb)calloc(1, sizeof(*q));
+    q->m = m;
+    unsigned int h_len = 4 * m + 1, i, j = 0;
+    float *h = (float *)malloc(h_len * sizeof(float));
+    ora_firdes_kaiser(h_len, 0.25f, fabsf(as), 0.0f, h);
+    for (i = 0; i < h_len; i++) {
+        float t = (float)i - (float)(h_len - 1) / 2.0f;
+        float complex hc = h[i] * cexpf(_Complex_I * 0.5f * M_PI * t);
+        h[i] = cimagf(hc);
+    }
+    q->hq = (float *)malloc(2 * m * sizeof(float));
+    for (i = 1; i < h_len; i += 2) q->hq[j++] = h[h_len - i - 1];
+    free(h);
+    win_init(&q->w, 4 * m, 2);
+    return q;
+}
+void ora_firhilb_destroy(ora_firhilb q)
+{
+    if (!q) return;
+    win_free(&q->w);
+    free(q->hq);
+    free(q);
+}
+void ora_firhilb_reset(ora_firhilb q) { win_reset(&q->w); }
+void ora_firhilb_get_taps(ora_firhilb q, float *hq) { memcpy(hq, q->hq, 2 * q->m * sizeof(float)); }
+
+/* firhilbf_c2r_execute(q, x, &y0 (lower sideband), &y1 (upper sideband)) */
+static inline void firhilb_c2r(ora_firhilb q, const float *x, float *y0, float *y1)
+{
+    win_push(&q->w, x);
+    const float *r = win_read(&q->w);          /* r[k] = x[n - 4m + 1 + k] */
+    const unsigned int m = q->m;
+    float xi[512], yq;
+    unsigned int j;
+    for (j = 0; j < 2 * m; j++) xi[j] = r[2 * (2 * j) + 1];
+    yq = dot_rr(q->hq, xi, 2 * m);
+    float yi = r[2 * (2 * m - 1)];
+    *y0 = yi + yq;
+    *y1 = yi - yq;
+}
+
+void ora_firhilb_c2r_block(ora_firhilb q, const float *x, size_t n, float *y0, float *y1)
+{
+    size_t i;
+    for (i = 0; i < n; i++) firhilb_c2r(q, x + 2 * i, y0 + i, y1 + i);
+}
+
+/* ===================================================================== */
 /* ampmodem: liquid src/modem/src/ampmodem.c (liquid >= 1.4)              */
 /* reference: src/demod.hpp:221-307; structure mirrored at demod.hpp:133  */
+/* demod per type (ampmodem_create's function pointer, as recalled):      */
+/*   dsb, carrier    ampmodem_demod_dsb_pll_carrier                       */
+/*   dsb, suppressed ampmodem_demod_dsb_pll_costas                        */
+/*   usb/lsb, carrier    ampmodem_demod_ssb_pll_carrier: the DSB carrier  */
+/*       PLL, then firhilbf_c2r(v1) -> (m_lsb, m_usb),                     */
+/*       m = 0.5f * m_sideband / mod_index, DC block                      */
+/*   usb/lsb, suppressed ampmodem_demod_ssb: firhilbf_c2r(x),             */
+/*       y = 0.5f * m_sideband / mod_index (no PLL, no DC block)          */
+/* SSB parity unpinned (recalled source, no liquid run to check against). */
 /* ===================================================================== */
 struct ora_ampmodem_s {
     float mod_index;
@@ -1524,6 +1603,7 @@ struct ora_ampmodem_s {
     unsigned int m;
     ora_nco mixer;
     ora_firfilt dcblock;       /* firfilt_rrrf_create_dc_blocker(m, 20) */
+    ora_firhilb hilbert;       /* firhilbf_create(m, 60) */
     ora_firfilt lowpass;       /* firfilt_crcf_create_kaiser(2m+1, 0.01, 40, 0) */
     float *delay;              /* wdelaycf(m): ring of m+1 samples */
     unsigned int dpos;
@@ -1531,7 +1611,7 @@ struct ora_ampmodem_s {
 
 ora_ampmodem ora_ampmodem_create(float mod_index, int type, int suppressed_carrier)
 {
-    if (type != 0) return NULL;   /* SSB modes: not restated in round 1 */
+    if (type < 0 || type > 2) return NULL;
     ora_ampmodem q = (ora_ampmodem)calloc(1, sizeof(*q));
     q->type = type;
     q->mod_index = mod_index;
@@ -1540,6 +1620,7 @@ ora_ampmodem ora_ampmodem_create(float mod_index, int type, int suppressed_carri
     q->mixer = ora_nco_create(0);
     ora_nco_pll_set_bandwidth(q->mixer, 0.001f);
     q->dcblock = ora_firfilt_create_dc_blocker(q->m, 20.0f, 0);
+    q->hilbert = ora_firhilb_create(q->m, 60.0f);
     q->lowpass = ora_firfilt_create_kaiser(2 * q->m + 1, 0.01f, 40.0f, 0.0f, 1);
     q->delay = (float *)calloc(2 * (q->m + 1), sizeof(float));
     ora_ampmodem_reset(q);
@@ -1550,6 +1631,7 @@ void ora_ampmodem_destroy(ora_ampmodem q)
     if (!q) return;
     ora_nco_destroy(q->mixer);
     ora_firfilt_destroy(q->dcblock);
+    ora_firhilb_destroy(q->hilbert);
     ora_firfilt_destroy(q->lowpass);
     free(q->delay);
     free(q);
@@ -1558,10 +1640,12 @@ void ora_ampmodem_reset(ora_ampmodem q)
 {
     ora_nco_reset(q->mixer);
     ora_firfilt_reset(q->dcblock);
+    ora_firhilb_reset(q->hilbert);
     ora_firfilt_reset(q->lowpass);
     memset(q->delay, 0, 2 * (q->m + 1) * sizeof(float));
     q->dpos = 0;
 }
+void ora_ampmodem_get_hilbert_taps(ora_ampmodem q, float *hq) { ora_firhilb_get_taps(q->hilbert, hq); }
 void ora_ampmodem_get_pll_state(ora_ampmodem q, uint32_t *theta, uint32_t *dtheta)
 {
     ora_nco_get_state(q->mixer, theta, dtheta);
@@ -1586,6 +1670,15 @@ static inline void wdelay_push_read(ora_ampmodem q, const float *x, float *out)
 void ora_ampmodem_demodulate_block(ora_ampmodem q, const float *x, size_t n, float *y)
 {
     size_t i;
+    if (q->type != 0 && q->suppressed_carrier) {
+        /* ampmodem_demod_ssb */
+        for (i = 0; i < n; i++) {
+            float lsb, usb;
+            firhilb_c2r(q->hilbert, x + 2 * i, &lsb, &usb);
+            y[i] = 0.5f * (q->type == 1 ? usb : lsb) / q->mod_index;
+        }
+        return;
+    }
     for (i = 0; i < n; i++) {
         float x0[2], x1[2], v0r, v0i, v1r, v1i, s, c;
         firfilt_push_exec(q->lowpass, x + 2 * i, x0);
@@ -1593,7 +1686,16 @@ void ora_ampmodem_demodulate_block(ora_ampmodem q, const float *x, size_t n, flo
         nco_sincos(q->mixer, &s, &c);
         cmul_down(x0[0], x0[1], c, s, &v0r, &v0i);
         cmul_down(x1[0], x1[1], c, s, &v1r, &v1i);
-        if (!q->suppressed_carrier) {
+        if (q->type != 0) {
+            /* ampmodem_demod_ssb_pll_carrier */
+            float phase_error = om_atan2f(v0i, v0r);           /* cargf(v0) */
+            ora_nco_pll_step(q->mixer, phase_error);
+            q->mixer->theta += q->mixer->d_theta;
+            float v1[2] = {v1r, v1i}, lsb, usb;
+            firhilb_c2r(q->hilbert, v1, &lsb, &usb);
+            float m = 0.5f * (q->type == 1 ? usb : lsb) / q->mod_index;
+            firfilt_push_exec(q->dcblock, &m, &y[i]);
+        } else if (!q->suppressed_carrier) {
             /* ampmodem_demod_dsb_pll_carrier */
             float phase_error = om_atan2f(v0i, v0r);           /* cargf(v0) */
             ora_nco_pll_step(q->mixer, phase_error);

@@ -133,8 +133,19 @@ void ora_ampmodem_destroy(ora_ampmodem q);
 void ora_ampmodem_reset(ora_ampmodem q);
 void ora_ampmodem_demodulate_block(ora_ampmodem q, const float *x, size_t n, float *y);
 void ora_ampmodem_get_pll_state(ora_ampmodem q, uint32_t *theta, uint32_t *dtheta);
-/* firfilt taps used inside (lowpass 2m+1 taps, dcblock 2m+1 taps, hilbert 4m+1) */
+/* firfilt taps used inside (lowpass 2m+1 taps, dcblock 2m+1 taps) */
 void ora_ampmodem_get_taps(ora_ampmodem q, float *lowpass, float *dcblock);
+/* the Hilbert transform's 2m quadrature taps (usb / lsb) */
+void ora_ampmodem_get_hilbert_taps(ora_ampmodem q, float *hq);
+
+/* ---- firhilbf (complex -> real) ---------------------------------------- */
+typedef struct ora_firhilb_s *ora_firhilb;
+ora_firhilb ora_firhilb_create(unsigned int m, float as);
+void ora_firhilb_destroy(ora_firhilb q);
+void ora_firhilb_reset(ora_firhilb q);
+void ora_firhilb_get_taps(ora_firhilb q, float *hq);
+/* y0: lower sideband retained, y1: upper sideband retained */
+void ora_firhilb_c2r_block(ora_firhilb q, const float *x, size_t n, float *y0, float *y1);
 
 /* ---- AMRadio chain (README.md:41-58) ---------------------------------- */
 typedef struct ora_amradio_s *ora_amradio;

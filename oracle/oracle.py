@@ -139,6 +139,12 @@ def _load():
         "ora_ampmodem_demodulate_block": (None, [vp, f32p, sz, f32p]),
         "ora_ampmodem_get_pll_state": (None, [vp, C.POINTER(u32), C.POINTER(u32)]),
         "ora_ampmodem_get_taps": (None, [vp, f32p, f32p]),
+        "ora_ampmodem_get_hilbert_taps": (None, [vp, f32p]),
+        "ora_firhilb_create": (vp, [u, f]),
+        "ora_firhilb_destroy": (None, [vp]),
+        "ora_firhilb_reset": (None, [vp]),
+        "ora_firhilb_get_taps": (None, [vp, f32p]),
+        "ora_firhilb_c2r_block": (None, [vp, f32p, sz, f32p, f32p]),
         "ora_amradio_create": (vp, [f, f, f, i]),
         "ora_amradio_destroy": (None, [vp]),
         "ora_amradio_max_out": (sz, [vp, sz]),
@@ -529,7 +535,7 @@ class AmpModem(_Handle):
         t = {"dsb": 0, "usb": 1, "lsb": 2}[type]
         self._h = lib().ora_ampmodem_create(mod_index, t, 0 if carrier else 1)
         if not self._h:
-            raise NotImplementedError("ampmodem: only DSB is restated")
+            raise ValueError("ampmodem: invalid configuration")
 
     def reset(self):
         lib().ora_ampmodem_reset(self._h)
@@ -546,11 +552,43 @@ class AmpModem(_Handle):
         lib().ora_ampmodem_get_taps(self._h, lp, dc)
         return lp, dc
 
+    def hilbert_taps(self):
+        h = np.zeros(50, np.float32)
+        lib().ora_ampmodem_get_hilbert_taps(self._h, h)
+        return h
+
     def __call__(self, x):
         xf = _c64_as_f32(x)
         y = np.empty(xf.size // 2, np.float32)
         lib().ora_ampmodem_demodulate_block(self._h, xf, xf.size // 2, y)
         return y
+
+
+class FirHilb(_Handle):
+    """firhilbf, complex -> real (c2r): returns (lower sideband, upper sideband)."""
+    _destroy = "ora_firhilb_destroy"
+
+    def __init__(self, m=25, As=60.0):
+        self.m = int(m)
+        self._h = lib().ora_firhilb_create(self.m, As)
+        if not self._h:
+            raise ValueError("firhilb: invalid configuration")
+
+    def reset(self):
+        lib().ora_firhilb_reset(self._h)
+
+    def taps(self):
+        h = np.zeros(2 * self.m, np.float32)
+        lib().ora_firhilb_get_taps(self._h, h)
+        return h
+
+    def c2r(self, x):
+        xf = _c64_as_f32(x)
+        n = xf.size // 2
+        y0 = np.empty(n, np.float32)
+        y1 = np.empty(n, np.float32)
+        lib().ora_firhilb_c2r_block(self._h, xf, n, y0, y1)
+        return y0, y1
 
 
 def deemphasis_coefs(sample_rate: float):

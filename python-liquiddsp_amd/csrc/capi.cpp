@@ -2,6 +2,7 @@
 // design and state bookkeeping, device staging, and dispatch to the gfx950
 // kernels.  No CPU fallback exists: every execute runs on a HIP device and
 // fails with LDSP_EHIP when none is present.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -39,6 +40,39 @@ double knob_env_f(const char* name, double dflt)
 const char* knob_env_s(const char* name) { return std::getenv(name); }
 #endif
 void set_last_error(const std::string& m) { g_last_error = m; }
+
+// roctx through dlopen (ldsp_common.hpp RoctxRange): resolved once; absent library -> no-ops
+namespace {
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+    Roctx()
+    {
+        void* h = nullptr;
+        for (const char* name : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                                 "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"}) {
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+        }
+        if (!h) return;
+        push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+        pop = (int (*)())dlsym(h, "roctxRangePop");
+        if (!push || !pop) push = nullptr, pop = nullptr;
+    }
+};
+const Roctx& roctx()
+{
+    static const Roctx r;
+    return r;
+}
+} // namespace
+void roctx_push(const char* m)
+{
+    if (roctx().push) roctx().push(m);
+}
+void roctx_pop()
+{
+    if (roctx().pop) roctx().pop();
+}
 
 int current_device()
 {
@@ -751,10 +785,13 @@ struct AmpObj {
     int type = 0;
     int suppressed = 1;
     unsigned int m = 25;
-    std::vector<float> lp, dc, table;
+    std::vector<float> lp, dc, hq, table;     // hq: the usb / lsb Hilbert transform's 2m quadrature taps
     k::AmpState st{};
     int device = -1;
     DevBuf dlp, ddc, dtab, dst, lph[2], dch[2];
+    // usb / lsb: Hilbert taps, its input history (4m - 1 samples, ping-pong) and per-slot v1 scratch
+    DevBuf dhq, hbh[2], v1[2];
+    int hcur = 0;
     // Per-call scratch in two slots (call parity) and the delay-line history in
     // three (call index mod 3), so that call k's front half (lowpass, history,
     // candidates) can run while call k-1's walker still reads its own slot.
@@ -807,6 +844,13 @@ struct AmpObj {
         for (auto& b : dlh) {
             b.ensure(m * 8, dev);
             zero_now(b.p, 0, m * 8);
+        }
+        if (!hq.empty()) {
+            upload(dhq, hq, dev);
+            for (auto& b : hbh) {
+                b.ensure((4 * m - 1) * 8, dev);
+                zero_now(b.p, 0, (4 * m - 1) * 8);
+            }
         }
         device = dev;
     }
@@ -1996,7 +2040,6 @@ int ldsp_ampmodem_create(float mod_index, int type, int suppressed_carrier, ldsp
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(type >= 0 && type <= 2, "ampmodem: type must be 0 (dsb), 1 (usb) or 2 (lsb)");
-        if (type != 0) throw Error(LDSP_EUNSUP, "ampmodem: single-sideband demodulation is not implemented");
         std::unique_ptr<ldsp_ampmodem_s> o(new ldsp_ampmodem_s());
         o->mod_index = mod_index;
         o->type = type;
@@ -2004,6 +2047,7 @@ int ldsp_ampmodem_create(float mod_index, int type, int suppressed_carrier, ldsp
         o->m = 25;
         o->lp = design::firdes_kaiser(2 * o->m + 1, 0.01f, 40.0f, 0.0f);   // carrier lowpass
         o->dc = design::firdes_notch(o->m, 0.0f, 20.0f);                     // DC blocker
+        if (type != 0) o->hq = design::firhilb_taps(o->m, 60.0f);            // firhilbf_create(m, 60)
         o->table = nco_table();
         o->reset_host();
         *q = o.release();
@@ -2030,12 +2074,27 @@ static void amp_reset(AmpObj* q)
     }
     for (auto& b : q->dlh)
         if (b.p) zero_now(b.p, 0, b.cap);
+    for (auto& b : q->hbh)
+        if (b.p) zero_now(b.p, 0, b.cap);
+    q->hcur = 0;
 }
 int ldsp_ampmodem_reset(ldsp_ampmodem_t q)
 {
     return guard([&] {
         NONNULL(q);
         amp_reset(q);
+    });
+}
+int ldsp_ampmodem_get_taps(ldsp_ampmodem_t q, float* lowpass, float* dcblock, float* hilbert)
+{
+    return guard([&] {
+        NONNULL(q);
+        if (lowpass) std::copy(q->lp.begin(), q->lp.end(), lowpass);
+        if (dcblock) std::copy(q->dc.begin(), q->dc.end(), dcblock);
+        if (hilbert) {
+            const std::vector<float> hq = q->hq.empty() ? design::firhilb_taps(q->m, 60.0f) : q->hq;
+            std::copy(hq.begin(), hq.end(), hilbert);
+        }
     });
 }
 int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
@@ -2099,7 +2158,8 @@ int ldsp_ampmodem_seq_stats(ldsp_ampmodem_t q, uint64_t* batches, uint64_t* redo
 // Costas: the candidates start from the true state (the loop's two stable
 // points half a turn apart make a guess ambiguous), so its front also waits for
 // call k-1's walk.
-static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, float mod_index, int costas, float* mbuf)
+static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, float mod_index, int costas, float* mbuf,
+                            int out_idx = 0)
 {
     const int L = 2 * (int)q->m + 1;
     const int sl = (int)(q->ncall & 1);
@@ -2122,6 +2182,7 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     c.table = q->dtab.as<float>();
     c.mod_index = mod_index;
     c.costas = costas;
+    c.out_idx = out_idx;
     c.alpha_host = q->st.alpha;
     c.y = mbuf;
     c.scratch = k::pll_parallel(n, costas) ? q->pll[sl].ensure(k::pll_scratch_bytes(n), q->device) : nullptr;
@@ -2157,6 +2218,38 @@ static void amp_call_end(AmpObj* q, const Exec& e)
     q->dev_newer = true;
 }
 
+// usb / lsb (liquid ampmodem_demod_ssb_pll_carrier / ampmodem_demod_ssb, see
+// oracle/liquid_restate.c).  Carrier: the DSB carrier PLL stage writes each
+// sample's table index, k_ssb_v1 recomputes v1 = delay(x) mixed down by it, the
+// Hilbert c2r keeps the sideband (0.5 * . / mod_index) and the DC blocker
+// follows.  Suppressed carrier: the Hilbert c2r of x alone.  The Hilbert history
+// is ordered across streams by `post` (like the DC blocker's).
+static void amp_ssb(AmpObj* q, const Exec& e, const void* dx, size_t n, float* dy)
+{
+    const int M = (int)q->m, H = 4 * M - 1, usb = q->type == 1 ? 1 : 0;
+    if (q->suppressed) {
+        q->post.wait(e.stream);
+        k::ssb_c2r(dx, q->hbh[q->hcur].p, n, q->dhq.as<float>(), M, usb, q->mod_index, dy, e.stream);
+        k::delay_hist(dx, q->hbh[q->hcur].p, q->hbh[1 - q->hcur].p, n, H, e.stream);
+        q->post.mark(e.stream);
+        q->hcur = 1 - q->hcur;
+        return;
+    }
+    const int L = 2 * M + 1;
+    const int sl = (int)(q->ncall & 1);
+    const void* dhist = q->dlh[q->ncall % 3].p;           // this call's delay-line history (read by the PLL stage too)
+    float* mbuf = amp_pll_stage(q, e, dx, n, q->mod_index, 0, nullptr, 1);
+    void* v1 = q->v1[sl].ensure(n * 8, q->device);
+    q->post.wait(e.stream);
+    k::ssb_v1(mbuf, dx, dhist, M, q->dtab.as<float>(), n, v1, e.stream);
+    k::ssb_c2r(v1, q->hbh[q->hcur].p, n, q->dhq.as<float>(), M, usb, q->mod_index, mbuf, e.stream);
+    k::delay_hist(v1, q->hbh[q->hcur].p, q->hbh[1 - q->hcur].p, n, H, e.stream);
+    k::fir_exact(false, mbuf, q->dch[q->cur].p, q->dch[1 - q->cur].p, n, q->ddc.as<float>(), L, 1.0f, dy, e.stream);
+    q->post.mark(e.stream);
+    q->hcur = 1 - q->hcur;
+    amp_call_end(q, e);
+}
+
 int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y, int mem, void* stream)
 {
     LDSP_RANGE("ldsp_ampmodem_demodulate");
@@ -2169,7 +2262,9 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
         const Exec e = make_exec(q->device, mem, stream, bd);
         const void* dx = q->stg.dev_in(e, x, n * 8);
         float* dy = (float*)q->stg.dev_out(e, y, n * 4);
-        if (n > 0) {
+        if (n > 0 && q->type != 0) {
+            amp_ssb(q, e, dx, n, dy);
+        } else if (n > 0) {
             const int L = 2 * (int)q->m + 1;
             float* mbuf = amp_pll_stage(q, e, dx, n, q->mod_index, q->suppressed ? 1 : 0, q->suppressed ? dy : nullptr);
             if (!q->suppressed) {

@@ -128,6 +128,26 @@ std::vector<float> firdes_notch(unsigned int m, float f0, float as)
     return h;
 }
 
+// firhilbf_create(m, As) (liquid firhilb.proto.c, as recalled): the 4m+1-tap
+// half-band kaiser prototype h turned into a Hilbert transformer,
+// h[i] = imag(h[i] e^{j pi t / 2}), t = i - 2m; C evaluates
+// cexpf(_Complex_I * 0.5f * M_PI * t) at the float (float)(0.5 pi t) and the
+// real * complex product's imaginary part is h[i] sinf(.), so the same here.
+// Returns the 2m odd taps, reversed: hq[j] = h[4m - 1 - 2j].
+std::vector<float> firhilb_taps(unsigned int m, float as)
+{
+    LDSP_REQUIRE(m >= 2, "firhilb: filter semi-length must be at least 2");
+    const unsigned int len = 4 * m + 1;
+    std::vector<float> h = firdes_kaiser(len, 0.25f, fabsf(as), 0.0f);
+    for (unsigned int i = 0; i < len; i++) {
+        const float t = (float)i - (float)(len - 1) / 2.0f;
+        h[i] = h[i] * sinf((float)(0.5 * kPi * (double)t));
+    }
+    std::vector<float> hq;
+    for (unsigned int i = 1; i < len; i += 2) hq.push_back(h[len - i - 1]);
+    return hq;
+}
+
 // ---------------------------------------------------------------- iirdes
 namespace {
 

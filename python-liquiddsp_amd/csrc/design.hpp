@@ -16,6 +16,8 @@ float kaiser(unsigned int i, unsigned int wlen, float beta);
 std::vector<float> firdes_kaiser(unsigned int n, float fc, float as, float mu);
 // liquid_firdes_notch(m, f0, as): 2m+1 taps
 std::vector<float> firdes_notch(unsigned int m, float f0, float as);
+// firhilbf_create(m, as): the 2m quadrature taps of the c2r Hilbert transform
+std::vector<float> firhilb_taps(unsigned int m, float as);
 
 struct SOS {
     std::vector<float> B, A;   // [nsos][3], a0 == 1

@@ -218,6 +218,53 @@ __global__ void __launch_bounds__(256) k_interleave2(const float* __restrict__ a
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) y[i] = make_float2(a[i], b[i]);
 }
 
+// AmpModem usb / lsb (liquid ampmodem_demod_ssb[_pll_carrier] -> firhilbf_c2r_execute,
+// see oracle/liquid_restate.c): v1 = x[n - m] mixed down by the PLL's table index
+// (cmul_down order), then per output
+//   yi = re z[n - 2M],  yq = sum_j hq[j] im z[n - 4M + 1 + 2j]  (sequential, oldest first)
+//   y  = 0.5f * (usb ? yi - yq : yi + yq) / mod_index
+// over z = the 4M - 1 samples of history ++ this call's input.
+__global__ void __launch_bounds__(256) k_ssb_v1(const uint32_t* __restrict__ idx, const float2* __restrict__ x,
+                                                const float2* __restrict__ dhist, int m, const float* __restrict__ tab,
+                                                long n, float2* __restrict__ v1)
+{
+    const long stride = (long)gridDim.x * 256;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const float2 u = i >= m ? x[i - m] : dhist[i];
+        const uint32_t k = idx[i] & 0x3ffu;
+        const float sn = tab[k], cs = tab[(k + 256) & 0x3ffu];
+        v1[i] = make_float2(u.x * cs - u.y * (-sn), u.x * (-sn) + u.y * cs);
+    }
+}
+
+constexpr int kHilTile = 1024;        // outputs per workgroup
+constexpr int kHilMaxM = 64;          // semi-length bound of the LDS tile
+
+__global__ void __launch_bounds__(256) k_ssb_c2r(const float2* __restrict__ x, const float2* __restrict__ hist, long n,
+                                                 const float* __restrict__ hq, int M, int usb, float mod_index,
+                                                 float* __restrict__ y)
+{
+    __shared__ float2 z[kHilTile + 4 * kHilMaxM];
+    __shared__ float h[2 * kHilMaxM];
+    const int H = 4 * M - 1;              // history samples
+    const long b0 = (long)blockIdx.x * kHilTile;
+    const int cnt = (int)min((long)kHilTile, n - b0);
+    for (int t = threadIdx.x; t < 2 * M; t += 256) h[t] = hq[t];
+    for (int t = threadIdx.x; t < cnt + H; t += 256) {
+        const long g = b0 - H + t;        // z index
+        z[t] = g >= 0 ? x[g] : hist[g + H];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < cnt; t += 256) {
+        // output b0 + t: z tile offset of sample n - k is t + H - k
+        const float yi = z[t + H - 2 * M].x;
+        float yq = 0.0f;
+        for (int j = 0; j < 2 * M; j++) yq += h[j] * z[t + 2 * j].y;
+        const float s = usb ? yi - yq : yi + yq;
+        y[b0 + t] = 0.5f * s / mod_index;
+    }
+}
+
 unsigned grid_for(size_t n) { return (unsigned)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 16384)); }
 
 } // namespace
@@ -240,6 +287,27 @@ void delay(bool cplx, const void* x, const void* hist, void* hist_out, size_t n,
     else
         hipLaunchKernelGGL(k_delay<float>, dim3(g), dim3(256), 0, s, (const float*)x, (const float*)hist,
                            (float*)hist_out, (long)n, D, (float*)y);
+    LDSP_HIP(hipGetLastError());
+}
+
+void ssb_v1(const void* idx, const void* x, const void* dhist, int m, const float* table, size_t n, void* v1,
+            hipStream_t s)
+{
+    if (n == 0) return;
+    LDSP_PROF(s, "k_ssb_v1");
+    hipLaunchKernelGGL(k_ssb_v1, dim3(grid_for(n)), dim3(256), 0, s, (const uint32_t*)idx, (const float2*)x,
+                       (const float2*)dhist, m, table, (long)n, (float2*)v1);
+    LDSP_HIP(hipGetLastError());
+}
+
+void ssb_c2r(const void* x, const void* hist, size_t n, const float* hq, int M, int usb, float mod_index, float* y,
+             hipStream_t s)
+{
+    if (n == 0) return;
+    LDSP_REQUIRE(M >= 2 && M <= kHilMaxM, "ssb_c2r: Hilbert semi-length out of range");
+    LDSP_PROF(s, "k_ssb_c2r");
+    hipLaunchKernelGGL(k_ssb_c2r, dim3((unsigned)((n + kHilTile - 1) / kHilTile)), dim3(256), 0, s, (const float2*)x,
+                       (const float2*)hist, (long)n, hq, M, usb, mod_index, y);
     LDSP_HIP(hipGetLastError());
 }
 

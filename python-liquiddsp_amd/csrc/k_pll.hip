@@ -52,6 +52,7 @@ struct PllIn {
     const float* table;
     float mod_index;
     int costas;
+    int out_idx;          // SSB carrier: the sample's table index (as float bits) is its output
 };
 
 __device__ __forceinline__ float2 x1_at(const PllIn& in, long n)
@@ -66,7 +67,7 @@ struct Kick {
     float out;
 };
 __device__ __forceinline__ Kick pll_eval(const float* tab, uint32_t i, float2 u0, float2 u1, float alpha, float beta,
-                                         float mod_index, int costas)
+                                         float mod_index, int costas, int out_idx)
 {
     const float sn = tab[i];
     const float cs = tab[(i + 256) & 0x3ffu];
@@ -77,7 +78,7 @@ __device__ __forceinline__ Kick pll_eval(const float* tab, uint32_t i, float2 u0
     Kick k;
     k.k1 = lm_constrain(phi * alpha);
     k.k2 = lm_constrain(phi * beta);
-    k.out = v1r / mod_index;
+    k.out = out_idx ? __uint_as_float(i) : v1r / mod_index;
     return k;
 }
 
@@ -104,7 +105,7 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
         __syncthreads();
         if (tid == 0) {
             for (int i = 0; i < cnt; i++) {
-                const Kick k = pll_eval(tab, tidx(theta), b0[i], b1[i], alpha, beta, in.mod_index, COSTAS ? 1 : 0);
+                const Kick k = pll_eval(tab, tidx(theta), b0[i], b1[i], alpha, beta, in.mod_index, COSTAS ? 1 : 0, in.out_idx);
                 d += k.k1;
                 theta += k.k2 + d;
                 y[base + i] = k.out;
@@ -136,7 +137,7 @@ struct SqCand {
 
 __device__ __forceinline__ SqCand sq_cands(const float2* b0, const float2* b1, int i0, int cnt, const float* tab,
                                            uint32_t theta, uint32_t d, uint32_t k1h, uint32_t k2h, float alpha,
-                                           float beta, float mod_index, int h0, int lane)
+                                           float beta, float mod_index, int out_idx, int h0, int lane)
 {
     const int j = lane / kSqCand;
     const uint32_t h = (uint32_t)(h0 + j);
@@ -154,7 +155,7 @@ __device__ __forceinline__ SqCand sq_cands(const float2* b0, const float2* b1, i
     const float phi = lm_atan2f_vsel(v0i, v0r);
     c.k1 = lm_constrain(phi * alpha);
     c.k2 = lm_constrain(phi * beta);
-    c.out = v1r / mod_index;
+    c.out = out_idx ? __uint_as_float(i) : v1r / mod_index;
     return c;
 }
 
@@ -183,11 +184,12 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
             const int nb = cnt / kSqBatch;
             SqCand cc{};
             uint32_t nredo = 0;
-            if (nb > 0) cc = sq_cands(b0, b1, 0, cnt, tab, theta, d, k1h, k2h, alpha, beta, in.mod_index, 0, lane);
+            if (nb > 0)
+                cc = sq_cands(b0, b1, 0, cnt, tab, theta, d, k1h, k2h, alpha, beta, in.mod_index, in.out_idx, 0, lane);
             for (int b = 0; b < nb; b++) {
                 const int i0 = b * kSqBatch;
                 const SqCand nx = sq_cands(b0, b1, i0 + kSqBatch, cnt, tab, theta, d, k1h, k2h, alpha, beta,
-                                           in.mod_index, kSqBatch, lane);
+                                           in.mod_index, in.out_idx, kSqBatch, lane);
                 // A sample whose index left its window is evaluated directly and the
                 // batch goes on from the state it gives (scripts/analysis/pll_predict.py:
                 // a third of the batches miss at horizons 4..7 on the bench signal, mostly
@@ -205,7 +207,8 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
                         o = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.out), ln));
                     } else {
                         miss = true;
-                        const Kick k = pll_eval(tab, tidx(theta), b0[i0 + j], b1[i0 + j], alpha, beta, in.mod_index, 0);
+                        const Kick k = pll_eval(tab, tidx(theta), b0[i0 + j], b1[i0 + j], alpha, beta, in.mod_index, 0,
+                                                    in.out_idx);
                         k1h = k.k1;
                         k2h = k.k2;
                         o = k.out;
@@ -218,7 +221,7 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
                 cc = nx;
             }
             for (int i = nb * kSqBatch; i < cnt; i++) {
-                const Kick k = pll_eval(tab, tidx(theta), b0[i], b1[i], alpha, beta, in.mod_index, 0);
+                const Kick k = pll_eval(tab, tidx(theta), b0[i], b1[i], alpha, beta, in.mod_index, 0, in.out_idx);
                 d += k.k1;
                 theta += k.k2 + d;
                 k1h = k.k1;
@@ -290,7 +293,7 @@ __device__ __forceinline__ void cand_step(const PllIn& in, const float* tab, lon
                                           const CandBuf& cb, uint4& rec, float& yo, uint32_t& nent)
 {
     const uint32_t ic = tidx(theta);
-    const Kick kc = pll_eval(tab, ic, c0, c1, alpha, beta, in.mod_index, in.costas);
+    const Kick kc = pll_eval(tab, ic, c0, c1, alpha, beta, in.mod_index, in.costas, in.out_idx);
     if (REC) {
         const uint32_t w = theta + (1u << 21);
         rec = make_uint4(w, kc.k1, kc.k2, __float_as_uint(kc.out));
@@ -570,7 +573,7 @@ __global__ void __launch_bounds__(256) k_pll_entries(PllIn in, const AmpState* s
         // the loop at the neighbouring table index (one cell up or down) minus the candidate's
         const uint32_t ic = w >> 22;
         const Kick kn = pll_eval(tab, (up ? ic + 1 : ic - 1) & 0x3ffu, in.x0[s], *x1_ptr(in, s), alpha, beta,
-                                 in.mod_index, in.costas);
+                                 in.mod_index, in.costas, in.out_idx);
         const uint32_t dk1 = kn.k1 - R0[r].y, dk2 = kn.k2 - R0[r].z;
         const uint32_t out = __float_as_uint(kn.out);
         // A repair here is right iff f_pre (the offset before it) lies in the
@@ -671,7 +674,7 @@ struct FullCtx {
     const float2* x;
     const float2* hist;
     const float* table;
-    int m, costas;
+    int m, costas, out_idx;
     float alpha, beta, mod_index;
 };
 
@@ -750,7 +753,7 @@ __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_
             const float2 u1 = make_float2(__uint_as_float(rl(__float_as_uint(q.u1.x), j)),
                                           __uint_as_float(rl(__float_as_uint(q.u1.y), j)));
             const Kick kt = pll_eval(tab, (ic + (vj >> 22)) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index,
-                                     fc.costas);
+                                     fc.costas, fc.out_idx);
             const uint32_t dk1 = rfl(kt.k1 - rl(q.r0.y, j));
             const uint32_t dk2 = rfl(kt.k2 - rl(q.r0.z, j));
             const uint32_t out = rfl(__float_as_uint(kt.out));
@@ -1164,6 +1167,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     fc.table = in.table;
     fc.m = in.m;
     fc.costas = in.costas;
+    fc.out_idx = in.out_idx;
     fc.alpha = st->alpha;
     fc.beta = st->beta;
     fc.mod_index = in.mod_index;
@@ -1363,6 +1367,7 @@ static PllIn pll_in(const PllCall& c)
     in.table = c.table;
     in.mod_index = c.mod_index;
     in.costas = c.costas;
+    in.out_idx = c.out_idx;
     return in;
 }
 

@@ -223,6 +223,8 @@ struct PllCall {
     const float* table;
     float mod_index;
     int costas;
+    int out_idx;          // 1: write each sample's table index (uint32 bits) instead of its output (SSB: the
+                          //    Hilbert stage recomputes v1 from it)
     float alpha_host;
     float* y;
     void* scratch;
@@ -247,6 +249,13 @@ void math_eval(int fn, const float* a, const float* b, float* y, size_t n, hipSt
 void bytes_to_iq(const void* x, void* y, size_t n, hipStream_t s);
 void delay(bool cplx, const void* x, const void* hist, void* hist_out, size_t n, int D, void* y, hipStream_t s);
 void freqdem(const void* x, const void* prev, void* prev_out, size_t n, float ref, float* y, hipStream_t s);
+// AmpModem usb / lsb: v1 = delay_m(x) mixed down by the per-sample table index idx
+// (the PLL stage's out_idx output); Hilbert c2r over x (4M - 1 samples of history
+// before x[0]) -> 0.5 * sideband / mod_index.
+void ssb_v1(const void* idx, const void* x, const void* dhist, int m, const float* table, size_t n, void* v1,
+            hipStream_t s);
+void ssb_c2r(const void* x, const void* hist, size_t n, const float* hq, int M, int usb, float mod_index, float* y,
+             hipStream_t s);
 struct FmState {          // FMStereo mixer loop state (device-resident)
     uint32_t theta, dtheta;
     float pe, alpha, beta;

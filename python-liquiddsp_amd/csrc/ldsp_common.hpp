@@ -10,7 +10,6 @@
 #include <string>
 
 #include "../../include/ldsp.h"
-#include <rocprofiler-sdk-roctx/roctx.h>
 
 namespace ldsp {
 
@@ -48,10 +47,14 @@ struct Scope {
 #define LDSP_PROF(stream, name) ::ldsp::prof::Scope LDSP_PROF_CAT(ldsp_prof_, __LINE__)((stream), (name))
 
 // roctx range around a C-ABI call (SURVEY section 5 tracing): visible in
-// `rocprofv3 --marker-trace`, a table lookup otherwise.
+// `rocprofv3 --marker-trace`.  librocprofiler-sdk-roctx is resolved with dlopen
+// on first use (capi.cpp), so the library loads and runs without it (the ranges
+// are then no-ops).
+void roctx_push(const char* m);
+void roctx_pop();
 struct RoctxRange {
-    explicit RoctxRange(const char* m) { roctxRangePushA(m); }
-    ~RoctxRange() { roctxRangePop(); }
+    explicit RoctxRange(const char* m) { roctx_push(m); }
+    ~RoctxRange() { roctx_pop(); }
     RoctxRange(const RoctxRange&) = delete;
     RoctxRange& operator=(const RoctxRange&) = delete;
 };

@@ -355,15 +355,13 @@ struct IIR {
         if (is_device_tensor(b)) {
             py::object& torch = torch_mod();
             py::object t = py::reinterpret_borrow<py::object>(b).attr("reshape")(-1).attr("contiguous")();
-            py::object dt = t.attr("dtype");
-            if (!(dt.equal(torch.attr("int16")) || dt.equal(torch.attr("uint8")) || dt.equal(torch.attr("int8"))))
-                throw py::value_error("from_bytes: the tensor must hold raw bytes or int16 samples (int16 / uint8 / int8)");
             py::object dev = t.attr("device");
             const int tdev = dev.attr("index").cast<int>();
             if (tdev != torch.attr("cuda").attr("current_device")().cast<int>())
                 throw py::value_error("input tensor is not on the current device");
+            // the tensor's raw bytes, whole (I, Q) pairs only: trailing 1-3 bytes are
+            // dropped, as bytes_to_iq does (utility.hpp:65 rounds size / 4 down)
             const size_t nbytes = t.attr("numel")().cast<size_t>() * t.attr("element_size")().cast<size_t>();
-            if (nbytes % 4) throw py::value_error("from_bytes: the input must hold whole (I, Q) int16 pairs (a multiple of 4 bytes)");
             if (reinterpret_cast<uintptr_t>(tptr(t)) % 4) t = t.attr("clone")();   // a view at an odd offset: the kernels read 4-byte pairs
             const size_t n = nbytes / 4;
             void* s = reinterpret_cast<void*>(
@@ -376,8 +374,7 @@ struct IIR {
         if (py::isinstance<py::array>(o)) o = py::module_::import("numpy").attr("ascontiguousarray")(o);
         py::buffer_info bi = py::reinterpret_borrow<py::buffer>(o).request();
         const size_t nbytes = (size_t)bi.size * (size_t)bi.itemsize;
-        if (nbytes % 4) throw py::value_error("from_bytes: the input must hold whole (I, Q) int16 pairs (a multiple of 4 bytes)");
-        const size_t n = nbytes / 4;
+        const size_t n = nbytes / 4;                  // trailing 1-3 bytes dropped, as bytes_to_iq
         py::array_t<cf> out(n);
         void* yp = out.mutable_data();
         int rc;
@@ -633,8 +630,7 @@ struct AmpModem {
     }
     // The setters rebuild the modem (state reset, demod.hpp:250-276).  The new
     // handle is created first and swapped in only on success, so a setter that
-    // fails (e.g. 'usb', not implemented) leaves the object and its settings
-    // unchanged instead of without a modem.
+    // fails leaves the object and its settings unchanged instead of without a modem.
     void set_type(const std::string& type)
     {
         if (type == "dsb" || type == "usb" || type == "lsb") make(mModulation, type, mCarrier);
@@ -663,6 +659,12 @@ struct AmpModem {
         uint32_t t, d;
         check(ldsp_ampmodem_get_pll_state(q, &t, &d));
         return py::make_tuple(t, d);
+    }
+    py::tuple taps()
+    {
+        py::array_t<float> lp(51), dc(51), hq(50);
+        check(ldsp_ampmodem_get_taps(q, lp.mutable_data(), dc.mutable_data(), hq.mutable_data()));
+        return py::make_tuple(lp, dc, hq);
     }
     py::tuple walk_stats()
     {
@@ -1049,6 +1051,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("reset", &AmpModem::reset)
         .def("pll_state", &AmpModem::pll_state)
         .def("_walk_stats", &AmpModem::walk_stats)
+        .def("_taps", &AmpModem::taps)
         .def("_seq_stats", &AmpModem::seq_stats)
         .def("__call__", &AmpModem::demod);
 

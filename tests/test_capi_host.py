@@ -284,3 +284,32 @@ def test_loop_fast_math_equals_general(lib, fn):
     checked, bad = C.c_uint64(), C.c_uint64()
     assert lib.ldsp_debug_math_fastcheck(fn, 0, 0xFFFFFFFF, 4099, C.byref(checked), C.byref(bad)) == 0
     assert checked.value > 100_000 and bad.value == 0, (checked.value, bad.value)
+
+
+@pytest.mark.parametrize("typ", ["dsb", "usb", "lsb"])
+def test_ampmodem_designs_bitwise(ld, ora, typ):
+    """AmpModem's designs (liquid ampmodem_create): the carrier lowpass, the DC
+    blocker and the usb / lsb Hilbert transform's quadrature taps
+    (firhilbf_create(25, 60)) are the restatement's, bit for bit."""
+    am = ld.AmpModem(modulation=0.5, type=typ, carrier=True)
+    assert am.type == typ
+    lp, dc, hq = am._taps()
+    o = ora.AmpModem(mod_index=0.5, type=typ, carrier=True)
+    olp, odc = o.taps()
+    assert (bits(lp) == bits(olp)).all() and (bits(dc) == bits(odc)).all()
+    assert (bits(hq) == bits(o.hilbert_taps())).all()
+    assert (bits(hq) == bits(ora.FirHilb(25, 60.0).taps())).all()
+
+
+def test_ampmodem_type_setter_accepts_ssb(ld):
+    """AmpModem.type = 'usb' / 'lsb' rebuilds the modem (demod.hpp:250-256); an
+    unknown type string leaves it unchanged."""
+    am = ld.AmpModem(modulation=0.5, type="dsb", carrier=False)
+    am.type = "usb"
+    assert am.type == "usb"
+    am.type = "lsb"
+    assert am.type == "lsb"
+    am.type = "ssb?"
+    assert am.type == "lsb"
+    am.carrier = True
+    assert (am.type, am.carrier) == ("lsb", True)

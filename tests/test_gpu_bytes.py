@@ -83,3 +83,22 @@ def test_from_bytes_real_filter_refused(ld):
     f = ld.RealIIRFilter(filter_type="cheby2", order=4, Fc=0.1)
     with pytest.raises(ValueError):
         f.from_bytes(np.zeros(8, np.int16))
+
+
+def test_from_bytes_odd_length_rounds_down(ld, rng):
+    # The reference's bytes_to_iq (utility.hpp:65) converts size / 4 whole (I, Q)
+    # pairs and drops 1-3 trailing bytes; from_bytes follows the same rule, so
+    # from_bytes(b) == self(bytes_to_iq(b)) for every length (host bytes and
+    # uint8 device tensors).
+    import torch
+    raw = raw_iq(rng, 5001).tobytes()
+    for extra in (b"", b"\x01", b"\x01\x02", b"\x01\x02\x03"):
+        a = ld.ComplexIIRFilter(**CHAIN_IIR)
+        b = ld.ComplexIIRFilter(**CHAIN_IIR)
+        ya = a.from_bytes(raw + extra)
+        yb = b(ld.bytes_to_iq(raw + extra))
+        assert ya.shape == (5001,) and np.array_equal(bits(ya), bits(yb))
+        t = torch.frombuffer(bytearray(raw + extra), dtype=torch.uint8).cuda()
+        a.reset()
+        b.reset()
+        assert torch.equal(a.from_bytes(t).view(torch.float32), b(ld.bytes_to_iq(t)).view(torch.float32))
