@@ -290,6 +290,11 @@ int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t *entries, uint64_t *rep
  * call: candidate batches stepped and batches redone directly because a table
  * index left its candidate window.  Synchronises. */
 int ldsp_ampmodem_seq_stats(ldsp_ampmodem_t q, uint64_t *batches, uint64_t *redone);
+/* Diagnostics, no reference counterpart: walker clock counters of the last
+ * chunk-parallel call (shader clocks spent walking / waiting at the per-block
+ * barrier), written only by the timing variants of a tuning build (zero
+ * otherwise).  Synchronises. */
+int ldsp_ampmodem_walk_clocks(ldsp_ampmodem_t q, uint64_t *walk, uint64_t *wait);
 /* Diagnostics, no reference counterpart: the walker's entry margin B = 2^log2_b
  * for the calls that follow (8..21; 0 restores the default).  A narrower
  * margin leaves fewer entries and fails more gap proofs, so more lane-blocks

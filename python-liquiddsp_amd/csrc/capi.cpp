@@ -179,31 +179,45 @@ struct PinnedBuf {
         return p;
     }
 };
-struct Staging {
-    static constexpr size_t kPinMax = (size_t)16 << 20;
-    DevBuf in, out;
+// Host staging of the numpy (host-buffer) path: pinned buffers shared by every
+// object a thread calls on one device (a host-buffer call is synchronous -- it
+// returns only after its output copy -- so a thread's calls never overlap in
+// them).  Grown on demand up to kPinMax each (larger transfers go unpinned), never
+// shrunk, and deliberately not freed at thread exit (hipHostFree at process
+// teardown can outlive the HIP runtime): at most 2 x kPinMax per thread and device.
+struct PinnedPool {
     PinnedBuf hin, hout;
     hipEvent_t hin_done = nullptr;    // the last copy out of hin (a call that threw may not have synchronized)
-    Staging() = default;
-    Staging(const Staging&) = delete;
-    Staging& operator=(const Staging&) = delete;
-    ~Staging() {
-        if (hin_done) (void)hipEventDestroy(hin_done);
-    }
     hipEvent_t done()
     {
         if (!hin_done) LDSP_HIP(hipEventCreateWithFlags(&hin_done, hipEventDisableTiming));
         return hin_done;
     }
+};
+static PinnedPool& pinned_pool(int device)
+{
+    thread_local std::vector<PinnedPool*> pools;
+    if ((int)pools.size() <= device) pools.resize(device + 1, nullptr);
+    if (!pools[device]) pools[device] = new PinnedPool();
+    return *pools[device];
+}
+
+struct Staging {
+    static constexpr size_t kPinMax = (size_t)16 << 20;
+    DevBuf in, out;                   // per object (device side)
+    Staging() = default;
+    Staging(const Staging&) = delete;
+    Staging& operator=(const Staging&) = delete;
     const void* dev_in(const Exec& e, const void* x, size_t bytes)
     {
         if (!e.host) return x;
         in.ensure(bytes, e.device);
         if (bytes && bytes <= kPinMax) {
-            LDSP_HIP(hipEventSynchronize(done()));
-            std::memcpy(hin.ensure(bytes), x, bytes);
-            LDSP_HIP(hipMemcpyAsync(in.p, hin.p, bytes, hipMemcpyHostToDevice, e.stream));
-            LDSP_HIP(hipEventRecord(hin_done, e.stream));
+            PinnedPool& pp = pinned_pool(e.device);
+            LDSP_HIP(hipEventSynchronize(pp.done()));
+            std::memcpy(pp.hin.ensure(bytes), x, bytes);
+            LDSP_HIP(hipMemcpyAsync(in.p, pp.hin.p, bytes, hipMemcpyHostToDevice, e.stream));
+            LDSP_HIP(hipEventRecord(pp.hin_done, e.stream));
         } else if (bytes) {
             LDSP_HIP(hipMemcpyAsync(in.p, x, bytes, hipMemcpyHostToDevice, e.stream));
         }
@@ -218,12 +232,13 @@ struct Staging {
     {
         if (!e.host) return;
         if (bytes && bytes <= kPinMax) {
-            LDSP_HIP(hipMemcpyAsync(hout.ensure(bytes), out.p, bytes, hipMemcpyDeviceToHost, e.stream));
+            PinnedPool& pp = pinned_pool(e.device);
+            LDSP_HIP(hipMemcpyAsync(pp.hout.ensure(bytes), out.p, bytes, hipMemcpyDeviceToHost, e.stream));
             // wait on an event (the host spins on it) rather than the stream, whose
             // synchronize may yield the thread: a README block makes five of these waits
-            LDSP_HIP(hipEventRecord(done(), e.stream));
-            LDSP_HIP(hipEventSynchronize(hin_done));
-            std::memcpy(y, hout.p, bytes);
+            LDSP_HIP(hipEventRecord(pp.done(), e.stream));
+            LDSP_HIP(hipEventSynchronize(pp.hin_done));
+            std::memcpy(y, pp.hout.p, bytes);
             return;
         }
         if (bytes) LDSP_HIP(hipMemcpyAsync(y, out.p, bytes, hipMemcpyDeviceToHost, e.stream));
@@ -2130,6 +2145,21 @@ int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t* entries, uint64_t* rep
         if (entries) *entries = stt[4];
         if (repairs) *repairs = stt[0];
         if (fallbacks) *fallbacks = stt[1];
+    });
+}
+
+int ldsp_ampmodem_walk_clocks(ldsp_ampmodem_t q, uint64_t* walk, uint64_t* wait)
+{
+    return guard([&] {
+        NONNULL(q);
+        unsigned long long stt[4] = {0, 0, 0, 0};
+        if (q->last_stats) {
+            DeviceGuard g(q->device);
+            q->sync_all();
+            LDSP_HIP(hipMemcpy(stt, q->last_stats, sizeof(stt), hipMemcpyDeviceToHost));
+        }
+        if (walk) *walk = stt[2];
+        if (wait) *wait = stt[3];
     });
 }
 

@@ -17,6 +17,7 @@
 //   span of its 64 outputs in LDS with coalesced loads.
 // NCO mix (nco_crcf_mix_block_{up,down}, reference src/nco.hpp:70,78):
 //   theta_i = theta_0 + i * dtheta (mod 2^32, exact), 1024-entry table in LDS.
+#include "resamp_dev.hpp"
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 
@@ -256,27 +257,6 @@ void fir_exact(bool cplx, const void* x, const void* hist, void* hist_out, size_
 
 // ====================================================================== resampler
 namespace {
-
-__device__ __forceinline__ long resamp_j(uint64_t P0, uint64_t k, uint32_t step)
-{
-    // smallest input index j with P0 + k*step - j*2^24 <= 0xffffff
-    const long long num = (long long)(P0 + k * (uint64_t)step) - 0xffffffLL;
-    return num <= 0 ? 0 : (long)((num + 0xffffffLL) >> 24);
-}
-
-// complex taps (cccf): C99 complex product, sequential accumulation
-__device__ __forceinline__ void rs_mac(float2& r, float2 h, float2 v)
-{
-    r.x = r.x + (h.x * v.x - h.y * v.y);
-    r.y = r.y + (h.x * v.y + h.y * v.x);
-}
-
-// real taps on complex samples (crcf): componentwise sequential accumulation
-__device__ __forceinline__ void rs_mac_cr(float2& r, float h, float2 v)
-{
-    r.x = r.x + h * v.x;
-    r.y = r.y + h * v.y;
-}
 
 template <bool CPLX, bool RT = false>
 __global__ void __launch_bounds__(64) k_resamp(const void* __restrict__ xv_, const void* __restrict__ hist_,

@@ -927,6 +927,10 @@ void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state,
 {
     if (n == 0) return;
     LDSP_REQUIRE(d.sos ? d.nsos <= kMaxSos : d.nv <= kMaxTf, "iir: filter order too high for the GPU kernels");
+    if (d.sos && d.nsos >= 1 && d.nsos <= kIirPipeMaxSos) {     // section-pipelined (k_iir_pipe.hip)
+        iir_pipe(cplx, d, x, n, state, y, s);
+        return;
+    }
     {
         LDSP_PROF(s, "k_iir_seq");
         const int z = iir_size_class(d);

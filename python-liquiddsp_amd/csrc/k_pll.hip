@@ -1052,7 +1052,19 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     "v_add_u32 " XN ", %[dk2], " XN "\n\t"                                                                 \
     "s_and_b64 %[mask], %[mask], %[above]\n\t"
 // lane-block Q: KC = lgkmcnt that has its own entries and the next one's E0 landed
-#define WB_LB(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN)                           \
+// (tuning-build timing variants, k_pll_walk VAR: bit 0 compares against ~0, so no
+// lane-block ever repairs (wrong output); bit 1 drops the per-lane-block store,
+// bit 2 the interval test; the product is VAR 0)
+#define WB_STORE(E1Z)                                                                                      \
+    "s_mov_b64 exec, %[pm]\n\t"                                                                            \
+    "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
+    "s_mov_b64 exec, -1\n\t"
+#define WB_TEST(E0W, E1W)                                                                                  \
+    "v_sub_u32 %[t], %[xp], " E0W "\n\t"                                                                   \
+    "v_cndmask_b32_e64 %[t], 0, %[t], %[pm]\n\t"                                                           \
+    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
+    "v_or_b32 %[acc], %[acc], %[t]\n\t"
+#define WB_LB_(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN, CMPW, STORE, TEST)           \
     "s_waitcnt lgkmcnt(" KC ")\n\t"                                                                        \
     "v_mul_lo_u32 %[t], %[d], " N0Z "\n\t"                                                                 \
     "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
@@ -1066,18 +1078,53 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
     WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc1 1b\n"                                           \
     "2:\n\t"                                                                                               \
-    "v_cmp_gt_u32_e64 %[mask], " XN ", " N0Y "\n\t"                                                        \
-    "v_sub_u32 %[t], %[xp], " E0W "\n\t"                                                                   \
-    "s_mov_b64 exec, %[pm]\n\t"                                                                            \
-    "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
-    "s_mov_b64 exec, -1\n\t"                                                                               \
-    "v_cndmask_b32_e64 %[t], 0, %[t], %[pm]\n\t"                                                           \
-    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
-    "v_or_b32 %[acc], %[acc], %[t]\n\t"                                                                    \
+    "v_cmp_gt_u32_e64 %[mask], " XN ", " CMPW "\n\t"                                                       \
+    STORE TEST                                                                                             \
     "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
     "s_add_u32 %[nrep], %[nrep], %[nr]\n\t"
+#define WB_LB(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN)                           \
+    WB_LB_(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN, N0Y, WB_STORE(E1Z), WB_TEST(E0W, E1W))
 #define WB_LBQ(Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN)                                            \
     WB_LB(Q, KC, "v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN)
+#ifdef LDSP_TUNING
+#define WB_LBV(Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, CMPW, STORE, TEST)                          \
+    WB_LB_(Q, KC, "v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, \
+           CMPW, STORE, TEST)
+#endif
+
+#define WB_READS                                                                                           \
+    "ds_read_b128 v[100:103], %[la]\n\t"                                                                   \
+    "ds_read_b128 v[104:107], %[la] offset:8192\n\t"                                                       \
+    "ds_read_b128 v[108:111], %[la] offset:1024\n\t"                                                       \
+    "ds_read_b128 v[112:115], %[la] offset:9216\n\t"                                                       \
+    "ds_read_b128 v[116:119], %[la] offset:2048\n\t"                                                       \
+    "ds_read_b128 v[120:123], %[la] offset:10240\n\t"                                                      \
+    "ds_read_b128 v[124:127], %[la] offset:3072\n\t"                                                       \
+    "ds_read_b128 v[128:131], %[la] offset:11264\n\t"                                                      \
+    "ds_read_b128 v[132:135], %[la] offset:4096\n\t"                                                       \
+    "ds_read_b128 v[136:139], %[la] offset:12288\n\t"                                                      \
+    "ds_read_b128 v[140:143], %[la] offset:5120\n\t"                                                       \
+    "ds_read_b128 v[144:147], %[la] offset:13312\n\t"                                                      \
+    "ds_read_b128 v[148:151], %[la] offset:6144\n\t"                                                       \
+    "ds_read_b128 v[152:155], %[la] offset:14336\n\t"                                                      \
+    "ds_read_b128 v[156:159], %[la] offset:7168\n\t"                                                       \
+    "ds_read_b128 v[160:163], %[la] offset:15360\n\t"                                                      \
+    "v_mov_b32 %[acc], 0\n\t"                                                                              \
+    "s_waitcnt lgkmcnt(15)\n\t"                                                                            \
+    "v_mul_lo_u32 %[t], %[d], v102\n\t"                                                                    \
+    "v_add3_u32 %[xa], v100, %[kb], %[t]\n\t"
+#define WB_OUTS                                                                                            \
+    : [xa] "=&v"(xa), [xb] "=&v"(xb), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [s7] "=&v"(srel7),     \
+      [mask] "=&s"(mask), [pm] "=&s"(pm), [bad] "=&s"(bad), [bit] "=&s"(bit), [above] "=&s"(above),           \
+      [kb] "+s"(Kb), [d] "+s"(D), [nrep] "+s"(nrep), [acc] "=&v"(acc),                                        \
+      [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr)
+#define WB_CLOBBERS                                                                                        \
+    : "scc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",  \
+      "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",   \
+      "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135",   \
+      "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148",   \
+      "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161",   \
+      "v162", "v163"
 
 // Returns nonzero when a repaired lane of the block failed its interval test.
 __device__ __forceinline__ bool walk_blk8(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep,
@@ -1086,6 +1133,219 @@ __device__ __forceinline__ bool walk_blk8(uint32_t lds, float* yb, uint32_t& Kb,
     uint32_t xa, xb, xp, t, off, acc, j, dk1, dk2, nr;
     unsigned long long mask, pm, bad, bit, above;
     asm volatile(
+        WB_READS
+        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n\t"
+        WB_LBQ("0", "13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]")
+        WB_LBQ("1", "11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]")
+        WB_LBQ("2", "9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]")
+        WB_LBQ("3", "7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]")
+        WB_LBQ("4", "5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]")
+        WB_LBQ("5", "3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]")
+        WB_LBQ("6", "1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]")
+        WB_LBQ("7", "0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]")
+        "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"
+        "v_mov_b32 %[s7], v158"
+        WB_OUTS
+        : [la] "v"(lds), [yb] "s"(yb)
+        WB_CLOBBERS);
+    return bad != 0;
+}
+
+#ifdef LDSP_TUNING
+// Timing variants of walk_blk8 (k_pll_walk VAR bits 0-2, see WB_LB_; wrong outputs).
+#define SEL_CMP_0(n1) n1
+#define SEL_CMP_1(n1) "%[ones]"
+#define SEL_ST_0(e1z) WB_STORE(e1z)
+#define SEL_ST_1(e1z) ""
+#define SEL_TE_0(e0w, e1w) WB_TEST(e0w, e1w)
+#define SEL_TE_1(e0w, e1w) ""
+#define WB_LBS(C, S, T, Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN)                                   \
+    WB_LBV(Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, SEL_CMP_##C("v" #n1), SEL_ST_##S("v" #g),      \
+           SEL_TE_##T("v" #d, "v" #h))
+#define DEF_WALK_BLK8(NAME, C, S, T)                                                                       \
+    __device__ __forceinline__ bool NAME(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep, \
+                                         uint32_t& srel7)                                                  \
+    {                                                                                                      \
+        uint32_t xa, xb, xp, t, off, acc, j, dk1, dk2, nr;                                                 \
+        unsigned long long mask, pm, bad, bit, above;                                                      \
+        const uint32_t ones = ~0u;                                                                         \
+        asm volatile(WB_READS "v_cmp_gt_u32_e64 %[mask], %[xa], " SEL_CMP_##C("v101") "\n\t"                 \
+                     WB_LBS(C, S, T, "0", "13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]") \
+                     WB_LBS(C, S, T, "1", "11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]") \
+                     WB_LBS(C, S, T, "2", "9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]") \
+                     WB_LBS(C, S, T, "3", "7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]") \
+                     WB_LBS(C, S, T, "4", "5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]") \
+                     WB_LBS(C, S, T, "5", "3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]") \
+                     WB_LBS(C, S, T, "6", "1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]") \
+                     WB_LBS(C, S, T, "7", "0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]") \
+                     "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"                                               \
+                     "v_mov_b32 %[s7], v158" WB_OUTS                                                       \
+                     : [la] "v"(lds), [yb] "s"(yb), [ones] "v"(ones) WB_CLOBBERS);                         \
+        return bad != 0;                                                                                   \
+    }
+DEF_WALK_BLK8(walk_blk8_v1, 1, 0, 0)
+DEF_WALK_BLK8(walk_blk8_v2, 0, 1, 0)
+DEF_WALK_BLK8(walk_blk8_v3, 1, 1, 0)
+DEF_WALK_BLK8(walk_blk8_v4, 0, 0, 1)
+DEF_WALK_BLK8(walk_blk8_v5, 1, 0, 1)
+DEF_WALK_BLK8(walk_blk8_v6, 0, 1, 1)
+DEF_WALK_BLK8(walk_blk8_v7, 1, 1, 1)
+#endif
+
+// Pipelined lane-block masks: each lane-block computes the NEXT lane-block's event
+// mask (MN) at its start from the carried offsets and again after every repair, so
+// the next lane-block's s_cmp reads a mask written many instructions earlier
+// instead of waiting for a v_cmp -> SALU hand-off at every lane-block boundary.
+#define WB_REP2(E1X, E1Y, SX, W, SXN, WN, X, XN, M, MN)                                                    \
+    "s_ff1_i32_b64 %[j], " M "\n\t"                                                                        \
+    "v_readlane_b32 %[dk1], " E1X ", %[j]\n\t"                                                             \
+    "v_readlane_b32 %[dk2], " E1Y ", %[j]\n\t"                                                             \
+    "s_lshl_b64 %[bit], 1, %[j]\n\t"                                                                       \
+    "s_lshl_b64 %[above], -2, %[j]\n\t"                                                                    \
+    "s_or_b64 %[pm], %[pm], %[bit]\n\t"                                                                    \
+    "v_mad_i32_i24 " X ", " SX ", %[dk1], " X "\n\t"                                                       \
+    "v_add_u32 " X ", %[dk2], " X "\n\t"                                                                   \
+    "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
+    "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
+    "v_cmp_gt_u32_e64 " M ", " X ", " W "\n\t"                                                             \
+    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
+    "v_mad_i32_i24 " XN ", " SXN ", %[dk1], " XN "\n\t"                                                    \
+    "v_add_u32 " XN ", %[dk2], " XN "\n\t"                                                                 \
+    "v_cmp_gt_u32_e64 " MN ", " XN ", " WN "\n\t"                                                          \
+    "s_and_b64 " M ", " M ", %[above]\n\t"
+#define WB_LB2(KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN, M, MN)                       \
+    "s_waitcnt lgkmcnt(" KC ")\n\t"                                                                        \
+    "v_mul_lo_u32 %[t], %[d], " N0Z "\n\t"                                                                 \
+    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
+    "v_lshlrev_b32 %[off], 2, " E0Z "\n\t"                                                                 \
+    "s_mov_b64 %[pm], 0\n\t"                                                                               \
+    "v_cmp_gt_u32_e64 " MN ", " XN ", " N0Y "\n\t"                                                         \
+    "s_cmp_eq_u64 " M ", 0\n\t"                                                                            \
+    "s_cbranch_scc1 2f\n"                                                                                  \
+    "1:\n\t"                                                                                               \
+    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc0 2f\n\t"                            \
+    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc0 2f\n\t"                            \
+    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc0 2f\n\t"                            \
+    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc1 1b\n"                              \
+    "2:\n\t"                                                                                               \
+    WB_STORE(E1Z) WB_TEST(E0W, E1W)                                                                        \
+    "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
+    "s_add_u32 %[nrep], %[nrep], %[nr]\n\t"
+#define WB_LB2Q(KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, M, MN)                                       \
+    WB_LB2(KC, "v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, M, MN)
+
+__device__ __forceinline__ bool walk_blk8_p(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep,
+                                            uint32_t& srel7)
+{
+    uint32_t xa, xb, xp, t, off, acc, j, dk1, dk2, nr;
+    unsigned long long mask, maskb, pm, bad, bit, above;
+    asm volatile(
+        WB_READS
+        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n\t"
+        WB_LB2Q("13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
+        WB_LB2Q("11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
+        WB_LB2Q("9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
+        WB_LB2Q("7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
+        WB_LB2Q("5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
+        WB_LB2Q("3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
+        WB_LB2Q("1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
+        WB_LB2Q("0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
+        "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"
+        "v_mov_b32 %[s7], v158"
+        WB_OUTS, [mb] "=&s"(maskb)
+        : [la] "v"(lds), [yb] "s"(yb)
+        WB_CLOBBERS);
+    return bad != 0;
+}
+
+template <int VAR>
+__device__ __forceinline__ bool walk_blk8_sel(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep,
+                                              uint32_t& srel7)
+{
+    if (VAR & 16) return walk_blk8_p(lds, yb, Kb, D, nrep, srel7);
+#ifdef LDSP_TUNING
+    switch (VAR & 7) {
+    case 1: return walk_blk8_v1(lds, yb, Kb, D, nrep, srel7);
+    case 2: return walk_blk8_v2(lds, yb, Kb, D, nrep, srel7);
+    case 3: return walk_blk8_v3(lds, yb, Kb, D, nrep, srel7);
+    case 4: return walk_blk8_v4(lds, yb, Kb, D, nrep, srel7);
+    case 5: return walk_blk8_v5(lds, yb, Kb, D, nrep, srel7);
+    case 6: return walk_blk8_v6(lds, yb, Kb, D, nrep, srel7);
+    case 7: return walk_blk8_v7(lds, yb, Kb, D, nrep, srel7);
+    default: break;
+    }
+#endif
+    return walk_blk8(lds, yb, Kb, D, nrep, srel7);
+}
+
+// ---- The walker's block loop as one asm statement (product path).  Per walker
+// block c (entries already in v100-v163, LB0's offsets / events carried in from
+// the previous block): the 8 lane-blocks of walk_blk8, each followed by the LDS
+// reads of the NEXT block's entries of that lane-block into its own registers
+// (free once it is done), so no block starts by waiting for the LDS; block
+// c + 1's header (its sample base) is read at the start of block c and its first
+// lane-block's offsets are formed in lane-block 7 (sxn = srel + S_{c+1} - S_c),
+// so the events of the next block's first lane-block are known when it starts.
+// Then the interval-test check (exit to the C++ fallback on failure, state of the
+// block's start in kb0 / d0 / nrep0), the rebase Kb += (S_{c+1} - S_c) D, the
+// barrier with the loader waves and the slot bookkeeping, all on SALU.  The
+// loaders guarantee blocks c + 1 and c + 2 landed at the barrier ending block c.
+// Repaired outputs are stored at y + 4 (S + srel) through a 32-bit offset
+// (n < 2^30 PCM samples per call, checked on the host).
+#define WL_PF(A, B, OFS_A, OFS_B)                                                                           \
+    "ds_read_b128 v[" #A "], %[ln] offset:" #OFS_A "\n\t"                                                  \
+    "ds_read_b128 v[" #B "], %[ln] offset:" #OFS_B "\n\t"
+// (the repaired lanes' store and interval test share one exec = PM window: the test
+// folds x_post - L' - span, saturated, into acc only in those lanes)
+#define WL_LB(E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, SXN, X, XN, TAIL)                           \
+    "v_mul_lo_u32 %[t], %[d], " SXN "\n\t"                                                                 \
+    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
+    "v_lshl_add_u32 %[off], " E0Z ", 2, %[s4]\n\t"                                                         \
+    "s_mov_b64 %[pm], 0\n\t"                                                                               \
+    "s_cmp_eq_u64 %[mask], 0\n\t"                                                                          \
+    "s_cbranch_scc1 2f\n"                                                                                  \
+    "1:\n\t"                                                                                               \
+    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
+    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
+    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
+    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc1 1b\n"                                           \
+    "2:\n\t"                                                                                               \
+    "v_cmp_gt_u32_e64 %[mask], " XN ", " N0Y "\n\t"                                                        \
+    "s_mov_b64 exec, %[pm]\n\t"                                                                            \
+    "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
+    "v_sub_u32 %[t], %[xp], " E0W "\n\t"                                                                   \
+    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
+    "v_or_b32 %[acc], %[acc], %[t]\n\t"                                                                    \
+    "s_mov_b64 exec, -1\n\t"                                                                               \
+    "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
+    "s_add_u32 %[nrep], %[nrep], %[nr]\n\t" TAIL
+#define WL_LBQ(a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, TAIL)                                              \
+    WL_LB("v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, TAIL)
+
+struct WalkLoop {
+    uint32_t c, kb, d, nrep;          // block index; offset model; live repair count
+    uint32_t kb0, d0, nrep0;          // at the start of block c (the fallback's entry state)
+    uint32_t S, Sprev;                // sample base of block c and of the last block completed here
+    uint32_t s7;                      // srel register of that block's lane-block 7 (fallback bookkeeping)
+};
+
+// Runs blocks c .. nblk - 1 until one fails its interval test (returns with c = that
+// block, not yet barriered) or all are done (c = nblk).
+__device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32_t ring, float* y, uint32_t lane16)
+{
+    constexpr uint32_t kSlot = (uint32_t)sizeof(WalkBufE);
+    static_assert(sizeof(WalkBufE) == 16400, "slot stride below");
+    const uint32_t rend = ring + kRing * kSlot;
+    const uint32_t la = ring + (w.c % kRing) * kSlot + lane16;        // block c's entries (prologue)
+    uint32_t sn = ring + ((w.c + 1) % kRing) * kSlot;                  // slot of block c + 1
+    uint32_t xa, xb, xp, t, off, acc, sx7, ln, lh, s7 = w.s7;
+    uint32_t j, dk1, dk2, nr, snx, dS, tS, s4;
+    unsigned long long mask, pm, bad, bit, above;
+    uint32_t kb = w.kb, d = w.d, nrep = w.nrep, c = w.c, S = w.S, Sprev = w.Sprev, kb0, d0, nrep0;
+    asm volatile(
+        // prologue: block c's entries, block c + 1's header, LB0's offsets / events
+        "v_mov_b32 %[lh], %[sn]\n\t"
+        "v_add_u32 %[ln], %[sn], %[l16]\n\t"
         "ds_read_b128 v[100:103], %[la]\n\t"
         "ds_read_b128 v[104:107], %[la] offset:8192\n\t"
         "ds_read_b128 v[108:111], %[la] offset:1024\n\t"
@@ -1102,38 +1362,97 @@ __device__ __forceinline__ bool walk_blk8(uint32_t lds, float* yb, uint32_t& Kb,
         "ds_read_b128 v[152:155], %[la] offset:14336\n\t"
         "ds_read_b128 v[156:159], %[la] offset:7168\n\t"
         "ds_read_b128 v[160:163], %[la] offset:15360\n\t"
+        "ds_read_b32 v164, %[lh] offset:16384\n\t"
+        "s_lshl_b32 %[s4], %[S], 2\n\t"
+        "s_mov_b32 %[kb0], %[kb]\n\t"
+        "s_mov_b32 %[d0], %[d]\n\t"
+        "s_mov_b32 %[nrep0], %[nrep]\n\t"
         "v_mov_b32 %[acc], 0\n\t"
-        "s_waitcnt lgkmcnt(15)\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
         "v_mul_lo_u32 %[t], %[d], v102\n\t"
         "v_add3_u32 %[xa], v100, %[kb], %[t]\n\t"
-        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n\t"
-        WB_LBQ("0", "13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]")
-        WB_LBQ("1", "11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]")
-        WB_LBQ("2", "9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]")
-        WB_LBQ("3", "7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]")
-        WB_LBQ("4", "5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]")
-        WB_LBQ("5", "3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]")
-        WB_LBQ("6", "1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]")
-        WB_LBQ("7", "0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]")
+        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n"
+        "9:\n\t"
+        WL_LBQ(100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]",
+               WL_PF(100:103, 104:107, 0, 8192))
+        WL_LBQ(108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]",
+               WL_PF(108:111, 112:115, 1024, 9216))
+        WL_LBQ(116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]",
+               WL_PF(116:119, 120:123, 2048, 10240))
+        WL_LBQ(124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]",
+               WL_PF(124:127, 128:131, 3072, 11264))
+        WL_LBQ(132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]",
+               WL_PF(132:135, 136:139, 4096, 12288))
+        WL_LBQ(140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]",
+               WL_PF(140:143, 144:147, 5120, 13312))
+        WL_LBQ(148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]",
+               WL_PF(148:151, 152:155, 6144, 14336))
+        // lane-block 7: its N0 is the next block's lane-block 0 (read after LB 0; the
+        // header of block c + 1 was the first read of this block)
+        "s_waitcnt lgkmcnt(13)\n\t"
+        "v_readfirstlane_b32 %[snx], v164\n\t"
+        "s_sub_u32 %[dS], %[snx], %[S]\n\t"
+        "v_add_u32 %[sx7], %[dS], v102\n\t"
+        WL_LB("v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v100", "v101", "%[sx7]", "%[xb]",
+              "%[xa]", "")
+        // block end
         "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"
-        "v_mov_b32 %[s7], v158"
-        : [xa] "=&v"(xa), [xb] "=&v"(xb), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [s7] "=&v"(srel7),
+        "s_mul_i32 %[tS], %[dS], %[d]\n\t"
+        "s_cmp_lg_u64 %[bad], 0\n\t"
+        "s_cbranch_scc1 8f\n\t"
+        "v_mov_b32 %[s7], v158\n\t"
+        WL_PF(156:159, 160:163, 7168, 15360)
+        "s_add_u32 %[kb], %[kb], %[tS]\n\t"
+        "s_mov_b32 %[Sp], %[S]\n\t"
+        "s_mov_b32 %[S], %[snx]\n\t"
+        "s_lshl_b32 %[s4], %[S], 2\n\t"
+        "s_mov_b32 %[kb0], %[kb]\n\t"
+        "s_mov_b32 %[d0], %[d]\n\t"
+        "s_mov_b32 %[nrep0], %[nrep]\n\t"
+        "v_mov_b32 %[acc], 0\n\t"
+        "s_add_u32 %[c], %[c], 1\n\t"
+        "s_add_u32 %[sn], %[sn], %[slot]\n\t"
+        "s_cmp_eq_u32 %[sn], %[rend]\n\t"
+        "s_cselect_b32 %[sn], %[ring], %[sn]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_barrier\n\t"
+        "v_mov_b32 %[lh], %[sn]\n\t"
+        "v_add_u32 %[ln], %[sn], %[l16]\n\t"
+        "ds_read_b32 v164, %[lh] offset:16384\n\t"
+        "s_cmp_lt_u32 %[c], %[nblk]\n\t"
+        "s_cbranch_scc1 9b\n"
+        "8:\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : [xa] "=&v"(xa), [xb] "=&v"(xb), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [acc] "=&v"(acc),
+          [sx7] "=&v"(sx7), [ln] "=&v"(ln), [lh] "=&v"(lh), [s7] "+v"(s7),
           [mask] "=&s"(mask), [pm] "=&s"(pm), [bad] "=&s"(bad), [bit] "=&s"(bit), [above] "=&s"(above),
-          [kb] "+s"(Kb), [d] "+s"(D), [nrep] "+s"(nrep), [acc] "=&v"(acc),
-          [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr)
-        : [la] "v"(lds), [yb] "s"(yb)
+          [kb] "+s"(kb), [d] "+s"(d), [nrep] "+s"(nrep), [c] "+s"(c), [S] "+s"(S), [Sp] "+s"(Sprev),
+          [kb0] "=&s"(kb0), [d0] "=&s"(d0), [nrep0] "=&s"(nrep0), [sn] "+s"(sn),
+          [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr), [snx] "=&s"(snx), [dS] "=&s"(dS),
+          [tS] "=&s"(tS), [s4] "=&s"(s4)
+        : [la] "v"(la), [l16] "v"(lane16), [nblk] "s"(nblk), [ring] "s"(ring), [rend] "s"(rend), [slot] "s"(kSlot),
+          [yb] "s"(y)
         : "scc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
           "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
           "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135",
           "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148",
           "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161",
-          "v162", "v163");
-    return bad != 0;
+          "v162", "v163", "v164");
+    w.c = c;
+    w.kb = kb;
+    w.d = d;
+    w.nrep = nrep;
+    w.kb0 = kb0;
+    w.d0 = d0;
+    w.nrep0 = nrep0;
+    w.S = S;
+    w.Sprev = Sprev;
+    w.s7 = s7;
 }
 
 // Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + kRing - 1
 // into the LDS ring meanwhile.
-template <bool F24, bool STATS>
+template <bool F24, bool STATS, int VAR = 0>
 __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, CandBuf cb,
                                                            float* __restrict__ y)
 {
@@ -1152,8 +1471,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     const long nblk = ((long)NE + kBlkE - 1) / kBlkE;
     if (wave != 0) {
         for (long b0 = 0; b0 < kRing - 1 && b0 < nblk; b0++) walk_dma(buf[b0], cb, b0, lw, lane);
-        // block 0 landed: at most the DMAs of blocks 1 .. kRing - 2 still in flight
-        vm_wait_blocks(nblk - 1);
+        // blocks 0 and 1 landed: at most the DMAs of blocks 2 .. kRing - 2 still in flight
+        vm_wait_blocks(min(5l, nblk - 2));
     }
     for (int i = tid; i < 1024; i += kWalkThreads) wtab[i] = in.table[i];
     __syncthreads();
@@ -1181,8 +1500,72 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     uint32_t S = 0;
     PrevLB prev{0u, 1, 0u, true};
     unsigned long long cyc_walk = 0, cyc_wait = 0;
-    for (long c = 0; c < nblk; c++) {
+    unsigned long long clk_walk = 0, clk_wait = 0;          // VAR & 8 (tuning): shader clocks
+    if constexpr (F24 && !STATS && VAR == 0) {
+        // the product path: the block loop in one asm statement (walk_asm_loop)
+        if (wave != 0) {
+            for (long c = 0; c < nblk; c++) {
+                // slot (c + kRing - 1) % kRing held block c - 1, released by the previous barrier
+                if (c + kRing - 1 < nblk) walk_dma(buf[(c + kRing - 1) % kRing], cb, c + kRing - 1, lw, lane);
+                // blocks c + 1 and c + 2 must have landed before the barrier ending block c
+                vm_wait_blocks(min(5l, nblk - c - 3));
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            }
+        } else {
+            WalkLoop w{0u, rfl(g.Kb), rfl(g.D), 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            const uint32_t ring = (uint32_t)(uintptr_t)&buf[0];
+            while (w.c < (uint32_t)nblk) {
+                const uint32_t c0 = w.c;
+                const uint32_t Sn = rfl(buf[c0 % kRing].hdr[0]);
+                w.kb += (Sn - w.S) * w.d;
+                w.S = Sn;
+                walk_asm_loop(w, (uint32_t)nblk, ring, y, (uint32_t)lane * 16u);
+                if (w.c > c0) prev = PrevLB{w.s7, 64, w.Sprev, false};
+                if (w.c >= (uint32_t)nblk) break;
+                // block c failed its interval test: undo its speculative stores (the
+                // candidates' outputs at every entry), then redo it lane-block by
+                // lane-block from its entry state (each rewrite lands after the previous one)
+                const long c = w.c;
+                const WalkBufE& b = buf[c % kRing];
+                const int cnt = (int)min((long)kBlkE, (long)NE - c * kBlkE);
+                S = w.S;
+                float* yb = y + S;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                for (int q = 0; q < kBlkE / 64; q++) {
+                    const uint32_t sr = b.e[0][q * 64 + lane].z;
+                    if (q * 64 + lane < cnt) y[S + sr] = __uint_as_float(cb.rec[(long)S + sr].w);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                g.Kb = w.kb0;
+                g.D = w.d0;
+                g.nrep = w.nrep0;
+                for (int q = 0; q < kBlkE / 64; q++) {
+                    const uint4 C0 = b.e[0][q * 64 + lane], C1 = b.e[1][q * 64 + lane];
+                    const uint4 N0 = b.e[0][min(q + 1, kBlkE / 64 - 1) * 64 + lane];
+                    uint32_t x = C0.x + g.Kb + C0.z * g.D;
+                    unsigned long long mk = __builtin_amdgcn_ballot_w64(x > C0.y);
+                    walk_lb24<false>(C0, C1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane, x, mk, N0.x,
+                                     N0.z, N0.y, yb);
+                }
+                w.kb = rfl(g.Kb);
+                w.d = rfl(g.D);
+                w.nrep = rfl(g.nrep);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                w.c++;
+            }
+            g.Kb = w.kb;
+            g.D = w.d;
+            g.nrep = w.nrep;
+            S = w.S;
+        }
+    }
+    for (long c = 0; c < ((F24 && !STATS && VAR == 0) ? 0 : nblk); c++) {
         const unsigned long long t0 = STATS ? wall_clock64() : 0;
+        const unsigned long long c0 = (VAR & 8) ? __builtin_amdgcn_s_memtime() : 0;
         if (wave != 0) {
             // slot (c + kRing - 1) % kRing held block c - 1, released by the previous barrier
             if (c + kRing - 1 < nblk) walk_dma(buf[(c + kRing - 1) % kRing], cb, c + kRing - 1, lw, lane);
@@ -1201,7 +1584,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 float* yb = y + S;
                 const uint32_t Kb0 = rfl(g.Kb), D0 = rfl(g.D), nrep0 = rfl(g.nrep);
                 uint32_t Kb = Kb0, D = D0, nrep = nrep0, s7;
-                const bool bad = walk_blk8((uint32_t)(uintptr_t)&b.e[0][lane], yb, Kb, D, nrep, s7);
+                const bool bad = walk_blk8_sel<VAR>((uint32_t)(uintptr_t)&b.e[0][lane], yb, Kb, D, nrep, s7);
                 g.Kb = Kb;
                 g.D = D;
                 g.nrep = nrep;
@@ -1263,9 +1646,15 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         // LDS-only barrier: __syncthreads() would also drain the loaders' global fetch of
         // block c + 2 (vmcnt(0)), putting an HBM round trip into every block
         const unsigned long long t1 = STATS ? wall_clock64() : 0;
+        const unsigned long long c1 = (VAR & 8) ? __builtin_amdgcn_s_memtime() : 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        if (VAR & 8) {
+            const unsigned long long c2 = __builtin_amdgcn_s_memtime();
+            clk_walk += c1 - c0;
+            clk_wait += c2 - c1;
+        }
         if (STATS) {
             const unsigned long long t2 = wall_clock64();
             cyc_walk += t1 - t0;
@@ -1281,6 +1670,10 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         cb.stats[0] = g.nrep;
         cb.stats[1] = g.nfb;
         cb.stats[4] = NE;
+        if (VAR & 8) {
+            cb.stats[2] = clk_walk;
+            cb.stats[3] = clk_wait;
+        }
         if (STATS) {
             cb.stats[2] = cyc_walk;
             cb.stats[3] = cyc_wait;
@@ -1473,10 +1866,28 @@ void pll_back(const PllCall& c, hipStream_t s)
     {
         LDSP_PROF(s, "k_pll_walk");
         static const bool stats = LDSP_KNOB("LDSP_DEBUG_PLL", 0) != 0;
+        // the walker stores repaired outputs through 32-bit byte offsets from y
+        LDSP_REQUIRE(c.n < (size_t(1) << 30), "ampmodem: at most 2^30 samples per call");
         const dim3 g(1), blk(kWalkThreads);
         const PllIn in = pll_in(c);
         const CandBuf cb = cand_buf(c);
         if (c.alpha_host <= 1.0f / 512.0f) {
+#ifdef LDSP_TUNING
+            // timing variants (k_pll_walk VAR): read per call
+            const int var = LDSP_KNOB("LDSP_WALK_VARIANT", 0);
+            if (!stats && var > 0) {
+#define WALK_VAR(V) case V: hipLaunchKernelGGL((k_pll_walk<true, false, V>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y); break;
+                switch (var) {
+                WALK_VAR(1) WALK_VAR(2) WALK_VAR(3) WALK_VAR(4) WALK_VAR(5) WALK_VAR(6) WALK_VAR(7)
+                WALK_VAR(8) WALK_VAR(9) WALK_VAR(10) WALK_VAR(11) WALK_VAR(12) WALK_VAR(13) WALK_VAR(14) WALK_VAR(15)
+                WALK_VAR(16) WALK_VAR(24)
+                default: break;
+                }
+#undef WALK_VAR
+                LDSP_HIP(hipGetLastError());
+                return;
+            }
+#endif
             if (stats) hipLaunchKernelGGL((k_pll_walk<true, true>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y);
             else hipLaunchKernelGGL((k_pll_walk<true, false>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y);
         } else {

@@ -78,6 +78,10 @@ struct IirDesc {
 // Sequential float32 evaluation (bit-exact with the liquid recursion).
 // state: float[2][3*nsos] (SOS) or float[2][nv] (TF); cplx -> 2 components.
 void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
+// The same recursion with one lane per (component, section), skewed two steps per
+// section (k_iir_pipe.hip); iir_seq uses it for SOS cascades of <= kIirPipeMaxSos.
+constexpr int kIirPipeMaxSos = 8;
+void iir_pipe(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
 // Float64 chunked linear scan.  state64: double[2][D] (the DF-II delay line in
 // the layout used by the scan); Apow: double[D*D] matrices: [0] = A^C,
 // [1 + l] = A^{C G 2^l} prepared by the host (see IirScanPlan).

@@ -672,6 +672,12 @@ struct AmpModem {
         check(ldsp_ampmodem_walk_stats(q, &e, &r, &f));
         return py::make_tuple(e, r, f);
     }
+    py::tuple walk_clocks()
+    {
+        uint64_t w, t;
+        check(ldsp_ampmodem_walk_clocks(q, &w, &t));
+        return py::make_tuple(w, t);
+    }
     py::tuple seq_stats()
     {
         uint64_t b, r;
@@ -1052,6 +1058,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("pll_state", &AmpModem::pll_state)
         .def("_walk_stats", &AmpModem::walk_stats)
         .def("_taps", &AmpModem::taps)
+        .def("_walk_clocks", &AmpModem::walk_clocks)
         .def("_seq_stats", &AmpModem::seq_stats)
         .def("__call__", &AmpModem::demod);
 

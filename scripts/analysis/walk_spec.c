@@ -184,6 +184,54 @@ int main(int argc, char** argv)
         if (!ok) jfail++;
         tot_pass_j += pj;
     }
+    /* sequential repair chain: at each repair j, is the next event (first lane > j
+     * with x > W) the same under the mask before this repair as after it? */
+    long steps = 0, same_next = 0;
+    for (long e0 = 0; e0 < nent; e0 += G) {
+        int g = nent - e0 < G ? (int)(nent - e0) : G;
+        uint32_t xv[4096];
+        for (int i = 0; i < g; i++) {
+            long s = es[e0 + i];
+            uint32_t ft = T[P + s] - C[s];
+            for (int r = 0; r < i; r++)
+                if (rep[e0 + r]) ft -= (uint32_t)tk2[e0 + r] + (uint32_t)(s - es[e0 + r]) * (uint32_t)tk1[e0 + r];
+            xv[i] = ft;
+        }
+        int j = -1;
+        for (;;) {
+            int nj = -1;
+            for (int i = j + 1; i < g; i++)
+                if ((u[e0 + i] + xv[i]) >= (1u << 22)) { nj = i; break; }
+            if (nj < 0) break;
+            /* repair at nj: the next event before / after applying it */
+            int before = -1, after = -1;
+            for (int i = nj + 1; i < g; i++)
+                if ((u[e0 + i] + xv[i]) >= (1u << 22)) { before = i; break; }
+            for (int i = nj + 1; i < g; i++)
+                xv[i] += (uint32_t)dk2[e0 + nj] + (uint32_t)(es[e0 + i] - es[e0 + nj]) * (uint32_t)dk1[e0 + nj];
+            for (int i = nj + 1; i < g; i++)
+                if ((u[e0 + i] + xv[i]) >= (1u << 22)) { after = i; break; }
+            steps++;
+            same_next += before == after;
+            j = nj;
+        }
+    }
+    printf("repair steps %ld: next event unchanged by the repair in %.1f %%\n", steps, 100.0 * same_next / steps);
+    /* |f| distribution over all samples (true vs candidate offset), and how many
+     * lane-blocks of 64 entries would have a gap endpoint beyond a narrower margin */
+    {
+        long cnt[24] = {0};
+        for (long s = 0; s < m; s++) {
+            int32_t fv = (int32_t)(T[P + s] - C[s]);
+            uint32_t a = fv < 0 ? -(uint32_t)fv : (uint32_t)fv;
+            int b = 0;
+            while (b < 23 && a >= (1u << (b + 1))) b++;
+            cnt[b]++;
+        }
+        printf("|f| over samples: ");
+        for (int b = 14; b < 23; b++) printf(">=2^%d: %.3f %%  ", b, 100.0 * ({long t = 0; for (int q = b; q < 24; q++) t += cnt[q]; t;}) / m);
+        printf("\n");
+    }
     printf("lane-blocks of %d: %ld, without repair %ld (%.1f %%), repairs per lane-block %.2f\n", G, nlb, lb0,
            100.0 * lb0 / nlb, (double)nrep / nlb);
     printf("prefix-fix passes per lane-block: mean %.3f; final set != repairs in %ld lane-blocks (multi-cell)\n",

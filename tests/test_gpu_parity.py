@@ -696,3 +696,38 @@ def test_device_tensor_path_matches_numpy(ld, ora, rng):
     r1 = ld.ComplexResampler(rate=0.024, Fc=0.024)
     r2 = ld.ComplexResampler(rate=0.024, Fc=0.024)
     assert_bitwise(r1(torch.from_numpy(x).cuda()).cpu().numpy(), r2(x))
+
+
+@pytest.mark.parametrize("cplx", [True, False])
+@pytest.mark.parametrize("order", [1, 2, 5, 8, 16])
+def test_iir_exact_pipeline_call_sizes(ld, ora, rng, cplx, order):
+    """Exact mode of an SOS cascade (k_iir_pipe: one lane per (component,
+    section), skewed two steps per section) across calls of every awkward
+    size: shorter than the skew, odd, one tile (2048 steps) +- 1, several tiles;
+    bit-identical to the sequential restatement and its state carried across."""
+    sizes = [1, 2, 3, 13, 14, 15, 2047, 2048, 2049, 4095, 6000, 3, 40_000]
+    n = sum(sizes)
+    x = cgauss(rng, n) if cplx else np.float32(rng.standard_normal(n))
+    cls = ld.ComplexIIRFilter if cplx else ld.RealIIRFilter
+    g = cls(filter_type="cheby2", order=order, Fc=np.float32(0.02))
+    g.exact = True
+    g._scan_path(1)              # never the speculative chunks: the sequential exact kernel
+    o = ora.IIRFilter(prototype=("cheby2", "lowpass", 1, order, np.float32(0.02), 0.3, 0.7, 60.0), cplx=cplx)
+    out, a = [], 0
+    for k in sizes:
+        out.append(g(x[a:a + k]))
+        a += k
+    assert_bitwise(np.concatenate(out), o(x))
+
+
+def test_iir_exact_chain_filter_large(ld, ora, rng):
+    """The chain's cheby2 order-8 band filter in exact mode on 4 Mi IQ samples in
+    one call (k_iir_pipe), bit-identical to the restatement."""
+    import torch
+    n = 1 << 22
+    x = cgauss(rng, n, 0.1)
+    g = ld.ComplexIIRFilter(**CHAIN_IIR)
+    g.exact = True
+    o = ora.IIRFilter(prototype=("cheby2", "lowpass", 1, 8, np.float32(0.0075), 0.3, 0.7, 60.0))
+    y = g(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert_bitwise(y, o(x))
