@@ -33,11 +33,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# One dependent repair of the PLL walk (s_ff1 -> 2 readlanes -> 24-bit multiply-add
-# -> compare -> s_and), the walker's own loop (unrolled x4) measured alone on MI355X by
-# scripts/ubench/walk_loop.hip (V8: 108.6 shader cycles at 2.39 GHz): the serial
-# floor of the walker per repair.
-REPAIR_FLOOR_NS = 45.4
+# One dependent repair of the PLL walk (s_ff1 -> exec = lanes above j, 2 readlanes ->
+# 24-bit multiply-add -> add -> compare into VCC -> VCCZ branch), the walker's own
+# loop (unrolled x4) measured alone on MI355X by scripts/ubench/walk_loop.hip (V10:
+# 89.0 shader cycles at 2.39 GHz, profiles/r04h_walk_loop.txt): the serial floor of
+# the walker per repair.  (Round 3's loop, V8: 108.6 cycles = 45.4 ns.)
+REPAIR_FLOOR_NS = 37.3
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector spec
 
 
@@ -513,6 +514,7 @@ def components(L, device, reps=5):
                             "fused_kernels": {k: round(v, 4) for k, v in tb.items()},
                             "alg_bytes_fused": 12 * n, "alg_bytes_two_calls": 24 * n}
     del raw
+    out["exact_chain_64Mi"] = exact_chain(L, device, n)
     n = 256 << 20
     xs = torch.complex(torch.randn(n, generator=g, device=device), torch.randn(n, generator=g, device=device))
     nco = L.NCO("nco")
@@ -539,6 +541,31 @@ def components(L, device, reps=5):
     out["host_buffers"] = host_path(L, device)
     out["channels_per_gpu"] = multi_channel(L, device)
     return out
+
+
+def exact_chain(L, device, n):
+    """The benchmarked chain with bandpass.exact = True -- the configuration whose
+    output is bit-identical to the restatement (tests/test_gpu_chain.py) -- one
+    64 Mi step on one stream.  Its cheby2 IIR is the float32 DF-II recursion run
+    in order (k_iir_pipe): float32 trajectories of this filter started early from
+    another state do not coalesce bit for bit (scripts/analysis/iir_coalesce.py,
+    DESIGN.md section 4), so no chunk-parallel exact form exists for it."""
+    x = synth_channel(n, 0, device)
+    r = AMRadio(L)
+    r.bandpass.exact = True
+    r(x[:65536])
+    torch.cuda.synchronize()
+    L._profile_reset()
+    L._profile_enable(True)
+    t0 = time.perf_counter()
+    r(x)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    L._profile_enable(False)
+    kern = {k: round(v[1] / v[0], 3) for k, v in L._profile_report().items()}
+    del x
+    return {"ms_per_step": round(el * 1e3, 2), "Msamples_s": round(n / el / 1e6, 2), "kernels_ms": kern,
+            "iir_kernel": "k_iir_pipe", "note": "exact (bit-identical) mode: the IIR is one sequential recursion"}
 
 
 def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False):

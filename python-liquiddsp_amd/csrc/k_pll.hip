@@ -517,13 +517,14 @@ __global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
 
 // Entry records, one wave per chunk (4 samples per lane).  Per entry (SoA per
 // walker block: E0[kBlkE], E1[kBlkE]), with srel = s - S_blk (< 2^17):
-//   E0 = (c, W, srel, L')
+//   E0 = (c, W, srel, L' - dk2)
 //        x = c + Kb + srel D = f(s) - lo; event iff x > W, [lo, lo + W] being
 //        the no-repair interval of f cut to [-B, B] when a neighbouring gap is
 //        non-empty (the gap to the previous / next entry)
 //   E1 = (dk1, dk2 - srel dk1, out, span) for the one crossing direction possible
 //        while |f| < 2^21 (up if u >= 2^21, else down); the repair was right iff
-//        x_post - L' <= span (see below).
+//        x_post - L' <= span (see below), i.e. x_pre - (L' - dk2) <= span with the
+//        offset before the repair (x_post = x_pre + dk2), which the walker keeps.
 // The tail of the last walker block is padded with W = ~0 (never an event).
 __global__ void __launch_bounds__(256) k_pll_entries(PllIn in, const AmpState* st, CandBuf cb, long n)
 {
@@ -595,7 +596,8 @@ __global__ void __launch_bounds__(256) k_pll_entries(PllIn in, const AmpState* s
         const uint32_t Lp = fl <= fh ? (uint32_t)(fl - lo) + dk2 : 0x80000000u;   // empty: always redo
         const uint32_t span = fl <= fh ? (uint32_t)(fh - fl) : 0u;
         uint4* E = cb.ent + (size_t)blk * 2 * kBlkE;
-        E[idx] = make_uint4(A - (uint32_t)lo, (uint32_t)(hi - lo), srel, Lp);
+        // stored as L' - dk2: the walker tests its pre-repair snapshot, x_pre = x_post - dk2
+        E[idx] = make_uint4(A - (uint32_t)lo, (uint32_t)(hi - lo), srel, Lp - dk2);
         E[kBlkE + idx] = make_uint4(dk1, dk2 - srel * dk1, out, span);
     }
     if (k == cb.nchc - 1) {              // pad the last walker block: events never fire there
@@ -806,8 +808,8 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
         if (F24) {
             // The repair chain, hand-scheduled (15 instructions; s_and sets SCC for
             // the back branch, no s_cmp): per repair j = ff1(mask); dk1, dk2' =
-            // lane j's (readlane); x += dk2' + srel dk1 in every lane; snapshot
-            // lane j's x; mask = events after j.  Exec is the full wave here.
+            // lane j's (readlane); snapshot lane j's x (pre-repair); x += dk2' +
+            // srel dk1 in every lane; mask = events after j.  Exec is the full wave here.
             uint32_t j, dk1, dk2;
             unsigned long long bit, above;
             asm volatile(
@@ -818,11 +820,11 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
                 "s_lshl_b64 %[bit], 1, %[j]\n\t"
                 "s_lshl_b64 %[above], -2, %[j]\n\t"
                 "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+                "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
                 "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
                 "v_add_u32 %[x], %[dk2], %[x]\n\t"
                 "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
                 "s_add_u32 %[d], %[d], %[dk1]\n\t"
-                "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
                 "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
                 "s_and_b64 %[mask], %[mask], %[above]\n\t"
                 "s_cbranch_scc1 1b"
@@ -836,14 +838,14 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
                 const uint32_t dk1 = rl(E1.x, j), dk2p = rl(E1.y, j);
                 const unsigned long long bit = 1ull << j;
                 PM |= bit;
+                xpost = sel_lane(xpost, x, bit);          // pre-repair offset (E0.w = L' - dk2)
                 x = mad_lane<F24>(sx, dk1, x) + dk2p;
-                xpost = sel_lane(xpost, x, bit);
                 D += dk1;
                 Kb += dk2p;
                 mask = __builtin_amdgcn_ballot_w64(x > E0.y) & ((~0ull << j) << 1);
             } while (mask != 0);
         }
-        // every repaired lane: x_post - L' <= span (E0.w, E1.w: k_pll_entries)
+        // every repaired lane: x_pre - (L' - dk2) <= span (E0.w, E1.w: k_pll_entries)
         unsigned long long bad = __builtin_amdgcn_ballot_w64(xpost - E0.w > E1.w) & PM;
         if (STATS && cb.dbg == 2) bad = 1;
         if (__builtin_expect(bad != 0, 0)) {
@@ -920,12 +922,12 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "s_lshl_b64 %[bit], 1, %[j]\n\t"
         "s_lshl_b64 %[above], -2, %[j]\n\t"
         "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
         "v_add_u32 %[x], %[dk2], %[x]\n\t"
         "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
         "s_add_u32 %[d], %[d], %[dk1]\n\t"
         "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
-        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
         "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
         "s_and_b64 %[mask], %[mask], %[above]\n\t"
@@ -936,12 +938,12 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "s_lshl_b64 %[bit], 1, %[j]\n\t"
         "s_lshl_b64 %[above], -2, %[j]\n\t"
         "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
         "v_add_u32 %[x], %[dk2], %[x]\n\t"
         "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
         "s_add_u32 %[d], %[d], %[dk1]\n\t"
         "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
-        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
         "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
         "s_and_b64 %[mask], %[mask], %[above]\n\t"
@@ -952,12 +954,12 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "s_lshl_b64 %[bit], 1, %[j]\n\t"
         "s_lshl_b64 %[above], -2, %[j]\n\t"
         "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
         "v_add_u32 %[x], %[dk2], %[x]\n\t"
         "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
         "s_add_u32 %[d], %[d], %[dk1]\n\t"
         "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
-        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
         "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
         "s_and_b64 %[mask], %[mask], %[above]\n\t"
@@ -968,12 +970,12 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "s_lshl_b64 %[bit], 1, %[j]\n\t"
         "s_lshl_b64 %[above], -2, %[j]\n\t"
         "s_or_b64 %[pm], %[pm], %[bit]\n\t"
+        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t"
         "v_add_u32 %[x], %[dk2], %[x]\n\t"
         "s_add_u32 %[kb], %[kb], %[dk2]\n\t"
         "s_add_u32 %[d], %[d], %[dk1]\n\t"
         "v_cmp_gt_u32_e64 %[mask], %[x], %[w]\n\t"
-        "v_cndmask_b32_e64 %[xp], %[xp], %[x], %[bit]\n\t"
         "v_mad_i32_i24 %[xn], %[sxn], %[dk1], %[xn]\n\t"
         "v_add_u32 %[xn], %[dk2], %[xn]\n\t"
         "s_and_b64 %[mask], %[mask], %[above]\n\t"
@@ -1042,12 +1044,12 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     "s_lshl_b64 %[bit], 1, %[j]\n\t"                                                                       \
     "s_lshl_b64 %[above], -2, %[j]\n\t"                                                                    \
     "s_or_b64 %[pm], %[pm], %[bit]\n\t"                                                                    \
+    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
     "v_mad_i32_i24 " X ", " SX ", %[dk1], " X "\n\t"                                                       \
     "v_add_u32 " X ", %[dk2], " X "\n\t"                                                                   \
     "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
     "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
     "v_cmp_gt_u32_e64 %[mask], " X ", " W "\n\t"                                                           \
-    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
     "v_mad_i32_i24 " XN ", " SXN ", %[dk1], " XN "\n\t"                                                    \
     "v_add_u32 " XN ", %[dk2], " XN "\n\t"                                                                 \
     "s_and_b64 %[mask], %[mask], %[above]\n\t"
@@ -1203,12 +1205,12 @@ DEF_WALK_BLK8(walk_blk8_v7, 1, 1, 1)
     "s_lshl_b64 %[bit], 1, %[j]\n\t"                                                                       \
     "s_lshl_b64 %[above], -2, %[j]\n\t"                                                                    \
     "s_or_b64 %[pm], %[pm], %[bit]\n\t"                                                                    \
+    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
     "v_mad_i32_i24 " X ", " SX ", %[dk1], " X "\n\t"                                                       \
     "v_add_u32 " X ", %[dk2], " X "\n\t"                                                                   \
     "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
     "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
     "v_cmp_gt_u32_e64 " M ", " X ", " W "\n\t"                                                             \
-    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
     "v_mad_i32_i24 " XN ", " SXN ", %[dk1], " XN "\n\t"                                                    \
     "v_add_u32 " XN ", %[dk2], " XN "\n\t"                                                                 \
     "v_cmp_gt_u32_e64 " MN ", " XN ", " WN "\n\t"                                                          \
@@ -1295,26 +1297,45 @@ __device__ __forceinline__ bool walk_blk8_sel(uint32_t lds, float* yb, uint32_t&
 #define WL_PF(A, B, OFS_A, OFS_B)                                                                           \
     "ds_read_b128 v[" #A "], %[ln] offset:" #OFS_A "\n\t"                                                  \
     "ds_read_b128 v[" #B "], %[ln] offset:" #OFS_B "\n\t"
-// (the repaired lanes' store and interval test share one exec = PM window: the test
-// folds x_post - L' - span, saturated, into acc only in those lanes)
+// Per repair (exec-masked): j = ff1(VCC); exec = the lanes above j; dk1, dk2' = lane
+// j's (readlane, which ignores exec); x += dk2' + srel dk1 in those lanes only; VCC =
+// their events (a VOPC writes 0 for inactive lanes, so VCC is already "events after
+// j": no s_and on the chain, and the loop branches on VCCZ).  Lane j itself keeps its
+// pre-repair offset, so after the loop the repaired lanes are exactly those whose x
+// is still > W (PM), and the interval test reads x_pre - (L' - dk2) <= span (E0.w).
+// No snapshot, no PM bookkeeping, no next-lane-block update inside the loop: the next
+// lane-block's offsets are formed once from the final Kb, D (v_mul_lo + v_add3) and
+// its events compared into VCC before this lane-block's store / test, which hide the
+// compare's latency before the next lane-block's VCCZ branch.
+#define WX_REP(E1X, E1Y, SX, W, X)                                                                         \
+    "s_ff1_i32_b64 %[j], vcc\n\t"                                                                          \
+    "s_lshl_b64 exec, -2, %[j]\n\t"                                                                        \
+    "v_readlane_b32 %[dk1], " E1X ", %[j]\n\t"                                                             \
+    "v_readlane_b32 %[dk2], " E1Y ", %[j]\n\t"                                                             \
+    "v_mad_i32_i24 " X ", " SX ", %[dk1], " X "\n\t"                                                       \
+    "v_add_u32 " X ", %[dk2], " X "\n\t"                                                                   \
+    "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
+    "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
+    "v_cmp_gt_u32_e32 vcc, " X ", " W "\n\t"
 #define WL_LB(E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, SXN, X, XN, TAIL)                           \
+    "s_cbranch_vccz 2f\n"                                                                                  \
+    "1:\n\t"                                                                                               \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccnz 1b\n"                                                    \
+    "3:\n\t"                                                                                               \
+    "s_mov_b64 exec, -1\n"                                                                                 \
+    "2:\n\t"                                                                                               \
     "v_mul_lo_u32 %[t], %[d], " SXN "\n\t"                                                                 \
     "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
+    "v_cmp_gt_u32_e64 %[pm], " X ", " E0Y "\n\t"                                                           \
     "v_lshl_add_u32 %[off], " E0Z ", 2, %[s4]\n\t"                                                         \
-    "s_mov_b64 %[pm], 0\n\t"                                                                               \
-    "s_cmp_eq_u64 %[mask], 0\n\t"                                                                          \
-    "s_cbranch_scc1 2f\n"                                                                                  \
-    "1:\n\t"                                                                                               \
-    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
-    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
-    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
-    WB_REP(E1X, E1Y, E0Z, E0Y, SXN, X, XN) "s_cbranch_scc1 1b\n"                                           \
-    "2:\n\t"                                                                                               \
-    "v_cmp_gt_u32_e64 %[mask], " XN ", " N0Y "\n\t"                                                        \
+    "v_sub_u32 %[t], " X ", " E0W "\n\t"                                                                   \
+    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
+    "v_cmp_gt_u32_e32 vcc, " XN ", " N0Y "\n\t"                                                            \
     "s_mov_b64 exec, %[pm]\n\t"                                                                            \
     "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
-    "v_sub_u32 %[t], %[xp], " E0W "\n\t"                                                                   \
-    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
     "v_or_b32 %[acc], %[acc], %[t]\n\t"                                                                    \
     "s_mov_b64 exec, -1\n\t"                                                                               \
     "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
@@ -1338,9 +1359,9 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
     const uint32_t rend = ring + kRing * kSlot;
     const uint32_t la = ring + (w.c % kRing) * kSlot + lane16;        // block c's entries (prologue)
     uint32_t sn = ring + ((w.c + 1) % kRing) * kSlot;                  // slot of block c + 1
-    uint32_t xa, xb, xp, t, off, acc, sx7, ln, lh, s7 = w.s7;
+    uint32_t xa, xb, t, off, acc, sx7, ln, lh, s7 = w.s7;
     uint32_t j, dk1, dk2, nr, snx, dS, tS, s4;
-    unsigned long long mask, pm, bad, bit, above;
+    unsigned long long pm, bad;
     uint32_t kb = w.kb, d = w.d, nrep = w.nrep, c = w.c, S = w.S, Sprev = w.Sprev, kb0, d0, nrep0;
     asm volatile(
         // prologue: block c's entries, block c + 1's header, LB0's offsets / events
@@ -1371,7 +1392,7 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
         "s_waitcnt lgkmcnt(0)\n\t"
         "v_mul_lo_u32 %[t], %[d], v102\n\t"
         "v_add3_u32 %[xa], v100, %[kb], %[t]\n\t"
-        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n"
+        "v_cmp_gt_u32_e32 vcc, %[xa], v101\n"
         "9:\n\t"
         WL_LBQ(100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]",
                WL_PF(100:103, 104:107, 0, 8192))
@@ -1423,16 +1444,16 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
         "s_cbranch_scc1 9b\n"
         "8:\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : [xa] "=&v"(xa), [xb] "=&v"(xb), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [acc] "=&v"(acc),
+        : [xa] "=&v"(xa), [xb] "=&v"(xb), [t] "=&v"(t), [off] "=&v"(off), [acc] "=&v"(acc),
           [sx7] "=&v"(sx7), [ln] "=&v"(ln), [lh] "=&v"(lh), [s7] "+v"(s7),
-          [mask] "=&s"(mask), [pm] "=&s"(pm), [bad] "=&s"(bad), [bit] "=&s"(bit), [above] "=&s"(above),
+          [pm] "=&s"(pm), [bad] "=&s"(bad),
           [kb] "+s"(kb), [d] "+s"(d), [nrep] "+s"(nrep), [c] "+s"(c), [S] "+s"(S), [Sp] "+s"(Sprev),
           [kb0] "=&s"(kb0), [d0] "=&s"(d0), [nrep0] "=&s"(nrep0), [sn] "+s"(sn),
           [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr), [snx] "=&s"(snx), [dS] "=&s"(dS),
           [tS] "=&s"(tS), [s4] "=&s"(s4)
         : [la] "v"(la), [l16] "v"(lane16), [nblk] "s"(nblk), [ring] "s"(ring), [rend] "s"(rend), [slot] "s"(kSlot),
           [yb] "s"(y)
-        : "scc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
+        : "scc", "vcc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
           "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
           "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135",
           "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148",

@@ -2,6 +2,7 @@
 // lane-block is an event (W = 0), so each lane-block runs 64 dependent repairs.
 // Reports device cycles (s_memtime) per repair for loop variants.
 //   hipcc --offload-arch=gfx950 -O3 walk_loop.hip -o walk_loop && ./walk_loop
+// V10 is the product loop since round 4 (k_pll.hip WX_REP); V8 the round-3 one.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -112,6 +113,34 @@ __global__ void __launch_bounds__(64) k_loop(const uint4* E, uint32_t* out, int 
                 asm volatile("1:\n\t" WL_BODY "s_cbranch_scc0 2f\n\t" WL_BODY "s_cbranch_scc0 2f\n\t" WL_BODY
                              "s_cbranch_scc0 2f\n\t" WL_BODY "s_cbranch_scc1 1b\n2:" WL_OPS);
             acc += xn;
+        } else if (V == 9 || V == 10) {   // exec-masked chain: the update runs only in the lanes
+            // above j (s_lshl exec), so the v_cmp's VCC is already "events after j": no s_and,
+            // the loop branches on VCCZ; no per-repair snapshot / PM (derived after the loop:
+            // the repaired lanes are those whose x is still > W, x holding their pre-repair offset)
+            uint32_t j, dk1, dk2;
+#define WX_BODY \
+    "s_ff1_i32_b64 %[j], vcc\n\t" \
+    "s_lshl_b64 exec, -2, %[j]\n\t" \
+    "v_readlane_b32 %[dk1], %[e1x], %[j]\n\t" \
+    "v_readlane_b32 %[dk2], %[e1y], %[j]\n\t" \
+    "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t" \
+    "v_add_u32 %[x], %[dk2], %[x]\n\t" \
+    "s_add_u32 %[kb], %[kb], %[dk2]\n\t" \
+    "s_add_u32 %[d], %[d], %[dk1]\n\t" \
+    "v_cmp_gt_u32_e32 vcc, %[x], %[w]\n\t"
+#define WX_OPS \
+    : [x] "+v"(x), [kb] "+s"(Kb), [d] "+s"(D), [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2) \
+    : [e1x] "v"(d1), [e1y] "v"(d2), [sx] "v"(sx), [w] "v"(W), [b] "s"(b) : "scc", "vcc", "exec"
+            if (V == 9)
+                asm volatile("v_add_u32 %[x], %[b], %[x]\n\tv_cmp_gt_u32_e32 vcc, %[x], %[w]\n\t"
+                             "s_cbranch_vccz 2f\n1:\n\t" WX_BODY "s_cbranch_vccnz 1b\n2:\n\ts_mov_b64 exec, -1" WX_OPS);
+            else
+                asm volatile("v_add_u32 %[x], %[b], %[x]\n\tv_cmp_gt_u32_e32 vcc, %[x], %[w]\n\t"
+                             "s_cbranch_vccz 2f\n1:\n\t" WX_BODY "s_cbranch_vccz 2f\n\t" WX_BODY "s_cbranch_vccz 2f\n\t"
+                             WX_BODY "s_cbranch_vccz 2f\n\t" WX_BODY "s_cbranch_vccnz 1b\n2:\n\ts_mov_b64 exec, -1" WX_OPS);
+            acc += x;
+            x = e.x;             // every lane an event again in the next lane-block
+            continue;
         } else if (V == 3) {     // pure SALU loop over the mask (no ballot per step)
             do {
                 const int j = __builtin_ctzll(mask);
@@ -155,6 +184,8 @@ int main()
     run(k_loop<6>, "V6 ds_bpermute broadcast");
     run(k_loop<7>, "V7 production asm, rolled");
     run(k_loop<8>, "V8 production asm, unrolled x4");
+    run(k_loop<9>, "V9 exec-masked, VCC branch, rolled");
+    run(k_loop<10>, "V10 exec-masked, VCC branch, unrolled x4");
     // s_memtime frequency: compare against wall clock
     hipEvent_t a, b;
     hipEventCreate(&a);

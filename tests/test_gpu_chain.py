@@ -107,3 +107,24 @@ def test_amradio_fast_within_policy(ld, ora):
     import os
     meta = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "variants.json")))
     assert dg["maxrel"] <= meta["chain_variant_spread_maxrel"], (dg, meta["chain_variant_spread_maxrel"])
+
+
+def test_amradio_exact_64Mi_bitwise(ld, ora):
+    """The exact chain (bandpass.exact = True: the configuration that is
+    bit-identical to the restatement) at the bench size: one 64 Mi-sample call
+    against the restatement on the same 64 Mi samples (~1 s on one host core),
+    bit for bit over all 1.6 M PCM samples."""
+    import torch
+    import bench
+    n = npre = 64 << 20
+    xd = bench.synth_channel(n, 0, torch.device("cuda", 0))
+    radio = bench.AMRadio(ld)
+    radio.bandpass.exact = True
+    y = radio(xd)
+    torch.cuda.synchronize()
+    assert y.numel() > 1_600_000
+    ref = ora.AMRadio()(xd[:npre].cpu().numpy())
+    assert ref.size == y.numel()
+    got = y.cpu().numpy()
+    eq = got.view(np.uint32) == ref.view(np.uint32)
+    assert eq.all(), f"{(~eq).sum()} of {eq.size} differ; first at {int(np.argmin(eq))}"
