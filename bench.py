@@ -69,7 +69,11 @@ def synth_channel(n, rank, device):
 class AMRadio:
     """The reference README's AMRadio callback, on the MI355X classes."""
 
-    def __init__(self, L, bandwidth=15000, iq_rate=2000000, pcm_rate=48000):
+    def __init__(self, L, bandwidth=15000, iq_rate=2000000, pcm_rate=48000, fused_front=False):
+        # fused_front: the IIR and the resampler as one call (liquiddsp.filter_resample,
+        # same bits; the filter's outputs stay on chip) -- the multi-channel component
+        self.L = L
+        self.fused_front = fused_front
         self.bandpass = L.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=bandwidth / iq_rate)
         self.resample = L.ComplexResampler(rate=pcm_rate / iq_rate, Fc=pcm_rate / iq_rate)
         self.am = L.AmpModem(modulation=0.5, type="dsb", carrier=True)
@@ -84,6 +88,11 @@ class AMRadio:
 
     def __call__(self, iq, events=None):
         x = iq
+        if self.fused_front and events is None:
+            x = self.L.filter_resample(self.bandpass, self.resample, x)
+            for st in (self.agc, self.am, self.audio_filter):
+                x = st(x)
+            return x
         for i, (_, st) in enumerate(self.stages()):
             if events is not None:
                 events[i][0].record()
@@ -539,7 +548,8 @@ def components(L, device, reps=5):
                                      "roof_ms": round(16 * n / HBM_PEAK_GBS / 1e6, 4)}
     del xs
     out["host_buffers"] = host_path(L, device)
-    out["channels_per_gpu"] = multi_channel(L, device)
+    out["channels_per_gpu"] = multi_channel(L, device, fused=True)
+    out["channels_per_gpu_unfused"] = multi_channel(L, device)
     return out
 
 
@@ -568,13 +578,13 @@ def exact_chain(L, device, n):
             "iir_kernel": "k_iir_pipe", "note": "exact (bit-identical) mode: the IIR is one sequential recursion"}
 
 
-def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False):
+def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False, fused=False):
     """SURVEY 8(e)'s caveat: independent channels also share one GPU -- each
     channel's serial PLL walk / AGC repair occupy one CU, so C channels on C
     stream pairs overlap.  Aggregate IQ Msamples/s of `channels` AMRadio chains
     (BASELINE config 4 each, carriers as the ranks of config 5) on this GPU."""
     xs = [synth_channel(n, r, device) for r in range(channels)]
-    radios = [AMRadio(L) for _ in range(channels)]
+    radios = [AMRadio(L, fused_front=fused) for _ in range(channels)]
     strm = [[torch.cuda.Stream(device) for _ in range(per)] for _ in range(channels)]
     # split: the front stages (IIR, resampler, AGC) and the back stages (AmpModem,
     # de-emphasis) of a step on different streams, so that stream order never
@@ -602,6 +612,7 @@ def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=Fals
     t = timed_steps(step, steps, max(2, per), torch.cuda.synchronize, lambda: None)
     del xs
     return {"channels": channels, "streams_per_channel": per * (2 if split else 1), "split_front_back": split,
+            "fused_front": fused,
             "steps": steps, "ms_per_step": round(t / steps * 1e3, 3),
             "Msamples_s": round(channels * n * steps / t / 1e6, 1),
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")}

@@ -220,6 +220,16 @@ int ldsp_iirfilt_execute(ldsp_iirfilt_t q, const void *x, size_t n, void *y, int
  * default fast mode) converts on load, so the input is read at 4 B per sample;
  * the exact and speculative paths convert with one extra pass first. */
 int ldsp_iirfilt_execute_iq16(ldsp_iirfilt_t q, const void *x, size_t n, void *y, int mem, void *stream);
+/* resamp(iirfilt(x)) in one call: the chain's first two stages (reference
+ * README.md:53-54, src/iirfilter.hpp:292-298 then src/resampler.hpp:160-172;
+ * an opt-in fusion, not a reference entry point).  y receives the resampler's
+ * outputs (*nout = ldsp_resamp_num_outputs(rs, n), at most cap), the same bits
+ * and the same state updates of both objects as ldsp_iirfilt_execute into a
+ * scratch buffer followed by ldsp_resamp_execute on it.  When the filter takes
+ * the modal scan (fast mode) the filter outputs never reach HBM; otherwise the
+ * two calls run.  Both objects complex (complex64) or both real. */
+int ldsp_iirfilt_resamp_execute(ldsp_iirfilt_t q, ldsp_resamp_t rs, const void *x, size_t n, void *y, size_t cap,
+                                size_t *nout, int mem, void *stream);
 
 /* ------------------------------------------------------------------------
  * AGC: agc_crcf.  Replaces AGC (src/agc.hpp:4-149).  execute implements

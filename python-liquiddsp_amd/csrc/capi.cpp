@@ -435,6 +435,7 @@ struct IirObj {
     uint32_t m_epoch = 0;
     int path_force = 0;               // ldsp_debug_iir_path: 0 auto, 1 blocked scan, 2 modal
     DevBuf iq;                        // int16 IQ converted for the paths that do not read it themselves
+    DevBuf rsside, rsbuf;             // ldsp_iirfilt_resamp_execute: unit edges (fused) / filter output (two calls)
     enum { kSt32 = 0, kSt64 = 1, kStModal = 2 };
     int state_at = kSt32;             // where the authoritative state lives
     int plan_C = 0;
@@ -447,6 +448,19 @@ struct IirObj {
 
     int fsz() const { return sos ? 3 * (int)nsos : nv; }
     int ncomp() const { return cplx ? 2 : 1; }
+    // which kernel path a call of n samples takes
+    enum Path { kSpec, kSeq, kModal, kBlk, kScan };
+    Path path_for(size_t n) const
+    {
+        // fast-decaying filters: speculative exact chunks (the sequential
+        // loop's bits, so exact mode takes them too: FMStereo's de-emphasis)
+        static const long spec_min = LDSP_KNOB("LDSP_IIR_SPEC_MIN", 0L);
+        if (D == 0) return kSeq;
+        if (path_force == 0 && spec_W > 0 && spec_W <= 16384 && (long)n >= spec_min) return kSpec;
+        if (mode == LDSP_MODE_EXACT) return kSeq;
+        if (mf.ok && path_force != 1) return kModal;
+        return D <= k::kIirBlkMaxD ? kBlk : kScan;
+    }
 
     // one step of the recursion on a state vector (the layout of the scan
     // kernels), in double or long double
@@ -1723,16 +1737,9 @@ static int iirfilt_execute(ldsp_iirfilt_t q, const void* x, size_t n, void* y, i
         void* dy = q->stg.dev_out(e, y, bytes);
         if (n > 0) {
             const k::IirDesc d = q->desc();
-            enum { kSpec, kSeq, kModal, kBlk, kScan } path;
-            // fast-decaying filters: speculative exact chunks (the sequential
-            // loop's bits, so exact mode takes them too: FMStereo's de-emphasis)
-            static const long spec_min = LDSP_KNOB("LDSP_IIR_SPEC_MIN", 0L);
-            if (q->D == 0) path = kSeq;
-            else if (q->path_force == 0 && q->spec_W > 0 && q->spec_W <= 16384 && (long)n >= spec_min) path = kSpec;
-            else if (q->mode == LDSP_MODE_EXACT) path = kSeq;
-            else if (q->mf.ok && q->path_force != 1) path = kModal;
-            else if (q->D <= k::kIirBlkMaxD) path = kBlk;
-            else path = kScan;
+            using P = IirObj::Path;
+            const P path = q->path_for(n);
+            enum { kSpec = P::kSpec, kSeq = P::kSeq, kModal = P::kModal, kBlk = P::kBlk, kScan = P::kScan };
             if (iq16 && path != kModal && path != kBlk) {   // not fused: convert first
                 void* cx = q->iq.ensure(n * 8, q->device);
                 k::bytes_to_iq(dx, cx, n, e.stream);
@@ -1792,6 +1799,80 @@ int ldsp_iirfilt_execute_iq16(ldsp_iirfilt_t q, const void* x, size_t n, void* y
 {
     LDSP_RANGE("ldsp_iirfilt_execute_iq16");
     return iirfilt_execute(q, x, n, y, mem, stream, true);
+}
+
+// IIR -> resampler (resamp(iirfilt(x))) in one pass when the filter takes the
+// modal scan: the filter outputs stay on chip (k_iir_modal<RS>), the resampler
+// outputs are the resampler kernels' bits, and both objects' states advance as
+// after the two calls.  Any other configuration runs the two calls.
+int ldsp_iirfilt_resamp_execute(ldsp_iirfilt_t q, ldsp_resamp_t rs, const void* x, size_t n, void* y, size_t cap,
+                                size_t* nout, int mem, void* stream)
+{
+    LDSP_RANGE("ldsp_iirfilt_resamp_execute");
+    return guard([&] {
+        NONNULL(q);
+        NONNULL(rs);
+        LDSP_REQUIRE(q->cplx == rs->cplx, "iirfilt_resamp_execute: the filter and the resampler must both be complex "
+                                          "or both real");
+        const size_t K = rs->num_outputs(n);
+        if (nout) *nout = K;
+        if (K > cap) throw Error(LDSP_ERANGE, "iirfilt_resamp_execute: output capacity too small");
+        LDSP_REQUIRE(n == 0 || x, "iirfilt_resamp_execute: NULL input");
+        LDSP_REQUIRE(K == 0 || y, "iirfilt_resamp_execute: NULL output");
+        const BufDevice bd(mem, x);
+        q->ensure_device();
+        rs->ensure_device();
+        LDSP_REQUIRE(q->device == rs->device, "iirfilt_resamp_execute: the filter and the resampler live on different "
+                                              "devices");
+        DeviceGuard g(q->device);
+        const Exec e = make_exec(q->device, mem, stream, bd);
+        const size_t es = q->cplx ? 8 : 4;
+        const bool fuse = n > 0 && q->path_for(n) == IirObj::kModal && rs->sub_len >= 2 &&
+                          rs->sub_len - 1 <= (unsigned)(64 * k::kIirModalChunk);
+        if (!fuse) {
+            auto ok = [](int rc) {
+                if (rc != LDSP_OK) throw Error(rc, ldsp_last_error());
+            };
+            if (e.host) {
+                std::vector<char> t(std::max<size_t>(n, 1) * es);
+                ok(ldsp_iirfilt_execute(q, x, n, t.data(), LDSP_MEM_HOST, nullptr));
+                ok(ldsp_resamp_execute(rs, t.data(), n, y, cap, nout, LDSP_MEM_HOST, nullptr));
+            } else {
+                void* t = q->rsbuf.ensure(std::max<size_t>(n, 1) * es, q->device);
+                ok(ldsp_iirfilt_execute(q, x, n, t, LDSP_MEM_DEVICE, stream));
+                ok(ldsp_resamp_execute(rs, t, n, y, cap, nout, LDSP_MEM_DEVICE, stream));
+                q->ord.mark(e.stream);            // the next filter call rewrites t only after the resampler read it
+            }
+            return;
+        }
+        q->ord.wait(e.stream);
+        rs->ord.wait(e.stream);
+        const void* dx = q->stg.dev_in(e, x, n * es);
+        void* dy = rs->stg.dev_out(e, y, K * es);
+        q->state_to(IirObj::kStModal, e.stream);
+        const k::IirModalPlan p = q->modal_plan(n);
+        k::IirResampFuse f;
+        f.sub = rs->dsub.as<float>();
+        f.P0 = rs->phase;
+        f.step = rs->step;
+        f.bits_index = rs->bits_index;
+        f.sub_len = (int)rs->sub_len;
+        f.ctaps = (rs->cplx && !rs->real_taps) ? 1 : 0;
+        f.K = (long)K;
+        f.side = (float*)q->rsside.ensure(k::iir_resamp_side_bytes(n, (int)rs->sub_len, q->cplx), q->device);
+        f.y = (float*)dy;
+        k::iir_modal_resamp(q->cplx, q->mf.cf, dx, n, q->mst.as<double>(), q->mstb.as<double>(), p, f,
+                            rs->hist[rs->cur].p, rs->hist[1 - rs->cur].p, e.stream);
+        std::swap(q->mst.p, q->mstb.p);
+        std::swap(q->mst.cap, q->mstb.cap);
+        rs->cur = 1 - rs->cur;
+        rs->phase = (uint64_t)((long long)rs->phase + (long long)K * rs->step - (long long)n * (1LL << 24));
+        q->ord.mark(e.stream);
+        rs->ord.mark(e.stream);
+        q->last = e.stream;
+        rs->last = e.stream;
+        rs->stg.finish(e, y, K * es);
+    });
 }
 
 // ---------------------------------------------------------------- AGC

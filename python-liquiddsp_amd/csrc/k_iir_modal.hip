@@ -41,6 +41,7 @@
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 #include "ldsp_math.hpp"
+#include "resamp_dev.hpp"
 
 namespace ldsp {
 namespace k {
@@ -195,8 +196,8 @@ __device__ __forceinline__ void comp_load(const void* __restrict__ xv, long n, l
 // read through the constant address space they are scalar loads.
 typedef const double __attribute__((address_space(4)))* cdptr;
 
-template <int M>
-__device__ __forceinline__ void modal_scan(const IirModalCoef& cf, const double* __restrict__ PSg, const float (&u)[kC],
+template <int M, typename U>
+__device__ __forceinline__ void modal_scan(const IirModalCoef& cf, const double* __restrict__ PSg, const U& u,
                                            int lane, Modal<M>& E)
 {
     const cdptr PS = (cdptr)PSg;
@@ -274,10 +275,11 @@ __device__ __forceinline__ void add_mat(const double* __restrict__ P, const Moda
 #ifndef LDSP_MODAL_WPE
 #define LDSP_MODAL_WPE 1
 #endif
-template <int NC, int M, bool IQ16>
+template <int NC, int M, bool IQ16, bool RS = false>
 __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalCoef cf, const void* __restrict__ xv, long n, long nw,
                                                        IirModalPlan p, const double* __restrict__ st_in,
-                                                       double* __restrict__ st_out, float* __restrict__ yv)
+                                                       double* __restrict__ st_out, float* __restrict__ yv,
+                                                       IirResampFuse f)
 {
     constexpr int kGran = M * 4;        // {half, epoch} granules per published component state
     __shared__ float pl[NC][64 * kRow];
@@ -443,25 +445,188 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
             st_out[(c * M + k) * 2] = z.w0[k];
             st_out[(c * M + k) * 2 + 1] = z.w1[k];
         }
+    if constexpr (RS) {
+        // the resampler on this unit's outputs, still in the planes (both
+        // components: complex taps mix them)
+        __syncthreads();
+        auto at = [&](int cc, long e) { return pl[cc][(e >> 5) * kRow + (e & 31)]; };
+        const int H = f.sub_len - 1;
+        const int hc = min(H, (int)cnt);
+        float* __restrict__ sd = f.side + (size_t)w * 2 * H * NC;
+        for (int t = lane; t < hc; t += 64) {
+            sd[t * NC + c] = at(c, t);                                  // head
+            sd[(2 * H - hc + t) * NC + c] = at(c, (long)cnt - hc + t);  // tail, right-aligned
+        }
+        const uint64_t kA = resamp_kmin(f.P0, wb + H, f.step);
+        const uint64_t kB = min((uint64_t)f.K, resamp_kmin(f.P0, wb + (long)cnt, f.step));
+        for (uint64_t k = kA + lane; k < kB; k += 64) {
+            const long j = resamp_j(f.P0, k, f.step);
+            const uint64_t ph = f.P0 + k * (uint64_t)f.step - ((uint64_t)j << 24);
+            const size_t b = (size_t)(ph >> f.bits_index);
+            const long e0 = j - H - wb;
+            float r = 0.0f;
+            if (NC == 2 && f.ctaps) {       // rs_mac: r.x += h.x v.x - h.y v.y, r.y += h.x v.y + h.y v.x
+                const float2* __restrict__ hb = reinterpret_cast<const float2*>(f.sub) + b * f.sub_len;
+                for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
+                    float2 h[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : make_float2(0.0f, 0.0f);
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (i0 + q < f.sub_len) {
+                            const float vr = at(0, e0 + i0 + q), vi = at(NC - 1, e0 + i0 + q);
+                            r = r + (c == 0 ? h[q].x * vr - h[q].y * vi : h[q].x * vi + h[q].y * vr);
+                        }
+                }
+            } else {                        // real taps: componentwise (rs_mac_cr / rrrf)
+                const float* __restrict__ hb = f.sub + b * f.sub_len;
+                for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
+                    float h[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : 0.0f;
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (i0 + q < f.sub_len) r = r + h[q] * at(c, e0 + i0 + q);
+                }
+            }
+            f.y[k * NC + c] = r;
+        }
+        return;
+    }
     __syncthreads();
     const __amdgpu_buffer_rsrc_t ry = unit_rsrc((const char*)yv + wb * kSout, cnt * kSout);
     if (vec) tile_store<NC, true>(ry, tid, pl);
     else tile_store<NC, false>(ry, tid, pl);
 }
 
-template <int NC, int M, bool IQ16>
+// One resampler output from a window in LDS (w0[i], w1[i]: component 0 / last of
+// sample i of the window), the resampler kernels' operations in their order; the
+// taps are read 8 at a time ahead of their use (one L2 round trip per 8 taps).
+template <int NC>
+__device__ __forceinline__ void rs_dot(const IirResampFuse& f, size_t b, const float* w0, const float* w1, int c,
+                                       float& r)
+{
+    if (NC == 2 && f.ctaps) {       // rs_mac: r.x += h.x v.x - h.y v.y, r.y += h.x v.y + h.y v.x
+        const float2* __restrict__ hb = reinterpret_cast<const float2*>(f.sub) + b * f.sub_len;
+        for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
+            float2 h[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : make_float2(0.0f, 0.0f);
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (i0 + q < f.sub_len) {
+                    const float vr = w0[i0 + q], vi = w1[i0 + q];
+                    r = r + (c == 0 ? h[q].x * vr - h[q].y * vi : h[q].x * vi + h[q].y * vr);
+                }
+        }
+    } else {                        // real taps: componentwise (rs_mac_cr / rrrf)
+        const float* __restrict__ hb = f.sub + b * f.sub_len;
+        const float* wc = c == 0 ? w0 : w1;
+        for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
+            float h[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : 0.0f;
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (i0 + q < f.sub_len) r = r + h[q] * wc[i0 + q];
+        }
+    }
+}
+
+// IIR -> resampler fusion, the outputs whose window straddles a unit boundary:
+// one workgroup per unit u stages the samples [wb - H, wb + H) (unit u - 1's tail,
+// or the resampler history before the call's first sample, and u's head) from
+// the side buffer into LDS and computes the outputs whose window ends in u's
+// first H samples; block 0 also writes the resampler's new history (the call's
+// last H filter outputs).  Same arithmetic and order as the resampler kernels.
+template <int NC>
+__global__ void __launch_bounds__(64) k_iir_resamp_edges(IirResampFuse f, long n, long nw,
+                                                         const float* __restrict__ hist, float* __restrict__ hist_out)
+{
+    extern __shared__ float win[];                  // [NC][2H]
+    const int H = f.sub_len - 1;
+    const int lane = threadIdx.x;
+    auto sample = [&](long g, int c) -> float {
+        if (g < 0) return hist[(g + H) * NC + c];
+        const long u = g / kUnit, o = g - u * kUnit;
+        const long cu = min((long)kUnit, n - u * kUnit);
+        const float* sd = f.side + (size_t)u * 2 * H * NC;
+        if (o < min((long)H, cu)) return sd[o * NC + c];
+        return sd[(H + o - cu + H) * NC + c];
+    };
+    const long u = blockIdx.x;
+    if (u == 0)
+        for (int t = lane; t < H; t += 64)
+            for (int c = 0; c < NC; c++) hist_out[t * NC + c] = sample(n - H + t, c);
+    const long wb = u * kUnit, cu = min((long)kUnit, n - wb);
+    const int span = H + (int)min((long)H, cu);
+    for (int t = lane; t < span; t += 64)
+        for (int c = 0; c < NC; c++) win[c * 2 * H + t] = sample(wb - H + t, c);
+    __syncthreads();
+    const uint64_t kA = resamp_kmin(f.P0, wb, f.step);
+    const uint64_t kB = min((uint64_t)f.K, resamp_kmin(f.P0, wb + min((long)H, cu), f.step));
+    for (uint64_t k = kA + lane; k < kB; k += 64) {
+        const long j = resamp_j(f.P0, k, f.step);
+        const uint64_t ph = f.P0 + k * (uint64_t)f.step - ((uint64_t)j << 24);
+        const size_t b = (size_t)(ph >> f.bits_index);
+        const int o = (int)(j - wb);                // the window's first sample, wb - H + o, sits at win[o]
+        for (int c = 0; c < NC; c++) {
+            float r = 0.0f;
+            rs_dot<NC>(f, b, win + o, win + (NC - 1) * 2 * H + o, c, r);
+            f.y[k * NC + c] = r;
+        }
+    }
+}
+
+template <int NC, int M, bool IQ16, bool RS = false>
 void launch_modal(const IirModalCoef& cf, const void* x, size_t n, const double* st_in, double* st_out,
-                  const IirModalPlan& p, float* y, hipStream_t s)
+                  const IirModalPlan& p, float* y, hipStream_t s, const IirResampFuse& f = IirResampFuse{})
 {
     const long nw = iir_modal_units(n);
-    LDSP_PROF(s, "k_iir_modal");
-    hipLaunchKernelGGL((k_iir_modal<NC, M, IQ16>), dim3((unsigned)(p.one_xcd ? 8 * nw : nw)), dim3(64 * NC), 0, s, cf,
-                       x, (long)n, nw, p, st_in, st_out, y);
+    LDSP_PROF(s, RS ? "k_iir_modal_rs" : "k_iir_modal");
+    hipLaunchKernelGGL((k_iir_modal<NC, M, IQ16, RS>), dim3((unsigned)(p.one_xcd ? 8 * nw : nw)), dim3(64 * NC), 0, s,
+                       cf, x, (long)n, nw, p, st_in, st_out, y, f);
 }
 
 } // namespace
 
 long iir_modal_units(size_t n) { return (long)((n + kUnit - 1) / kUnit); }
+
+size_t iir_resamp_side_bytes(size_t n, int sub_len, bool cplx)
+{
+    return (size_t)iir_modal_units(n) * 2 * std::max(sub_len - 1, 1) * (cplx ? 2 : 1) * sizeof(float);
+}
+
+void iir_modal_resamp(bool cplx, const IirModalCoef& cf, const void* x, size_t n, const double* st_in,
+                      double* st_out, const IirModalPlan& p, const IirResampFuse& f, const void* hist,
+                      void* hist_out, hipStream_t s)
+{
+    if (n == 0) return;
+    LDSP_REQUIRE(cf.M >= 1 && cf.M <= kIirModalMax, "iir: modal form with 1..8 modes");
+    LDSP_REQUIRE(p.J >= 1 && p.J <= kIirModalJmax, "iir: look-back depth out of range");
+    LDSP_REQUIRE(f.sub_len >= 2 && f.sub_len - 1 <= kUnit, "iir_resamp: resampler window of 2 .. 2049 samples");
+#define LDSP_MODAL(MM)                                                                                        \
+    case MM:                                                                                                  \
+        if (cplx) launch_modal<2, MM, false, true>(cf, x, n, st_in, st_out, p, nullptr, s, f);                \
+        else launch_modal<1, MM, false, true>(cf, x, n, st_in, st_out, p, nullptr, s, f);                     \
+        break;
+    switch (cf.M) {
+        LDSP_MODAL(1) LDSP_MODAL(2) LDSP_MODAL(3) LDSP_MODAL(4) LDSP_MODAL(5) LDSP_MODAL(6) LDSP_MODAL(7) LDSP_MODAL(8)
+    default: throw Error(LDSP_EUNSUP, "iir: unsupported number of modes");
+    }
+#undef LDSP_MODAL
+    LDSP_HIP(hipGetLastError());
+    const long nw = iir_modal_units(n);
+    LDSP_PROF(s, "k_iir_resamp_edges");
+    const size_t lds = (size_t)(cplx ? 2 : 1) * 2 * (f.sub_len - 1) * sizeof(float);
+    if (cplx)
+        hipLaunchKernelGGL(k_iir_resamp_edges<2>, dim3((unsigned)nw), dim3(64), lds, s, f, (long)n, nw,
+                           (const float*)hist, (float*)hist_out);
+    else
+        hipLaunchKernelGGL(k_iir_resamp_edges<1>, dim3((unsigned)nw), dim3(64), lds, s, f, (long)n, nw,
+                           (const float*)hist, (float*)hist_out);
+    LDSP_HIP(hipGetLastError());
+}
 
 void iir_modal(bool cplx, const IirModalCoef& cf, const void* x, size_t n, const double* st_in, double* st_out,
                const IirModalPlan& p, void* y, hipStream_t s, bool iq16)

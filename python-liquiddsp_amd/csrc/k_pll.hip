@@ -1340,8 +1340,139 @@ __device__ __forceinline__ bool walk_blk8_sel(uint32_t lds, float* yb, uint32_t&
     "s_mov_b64 exec, -1\n\t"                                                                               \
     "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
     "s_add_u32 %[nrep], %[nrep], %[nr]\n\t" TAIL
-#define WL_LBQ(a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, TAIL)                                              \
-    WL_LB("v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, TAIL)
+#ifdef LDSP_TUNING
+// Timing variants of the product loop (tuning build, k_pll_walk VAR 32 / 64; wrong
+// outputs): NOREP skips every repair loop (the lane-block transitions, stores and
+// tests alone), NOST drops the store / interval test / repair count (loop + transitions).
+#define WL_LB_NOREP(E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, SXN, X, XN, TAIL)                     \
+    "s_branch 2f\n"                                                                                        \
+    "2:\n\t"                                                                                               \
+    "v_mul_lo_u32 %[t], %[d], " SXN "\n\t"                                                                 \
+    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
+    "v_cmp_gt_u32_e64 %[pm], " X ", " E0Y "\n\t"                                                           \
+    "v_lshl_add_u32 %[off], " E0Z ", 2, %[s4]\n\t"                                                         \
+    "v_sub_u32 %[t], " X ", " E0W "\n\t"                                                                   \
+    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
+    "v_cmp_gt_u32_e32 vcc, " XN ", " N0Y "\n\t"                                                            \
+    "s_mov_b64 exec, %[pm]\n\t"                                                                            \
+    "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
+    "s_mov_b64 exec, -1\n\t"                                                                               \
+    "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
+    "s_add_u32 %[nrep], %[nrep], %[nr]\n\t" TAIL
+#define WL_LB_NOST(E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, SXN, X, XN, TAIL)                      \
+    "s_cbranch_vccz 2f\n"                                                                                  \
+    "1:\n\t"                                                                                               \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccnz 1b\n"                                                    \
+    "3:\n\t"                                                                                               \
+    "s_mov_b64 exec, -1\n"                                                                                 \
+    "2:\n\t"                                                                                               \
+    "v_mul_lo_u32 %[t], %[d], " SXN "\n\t"                                                                 \
+    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
+    "v_cmp_gt_u32_e32 vcc, " XN ", " N0Y "\n\t" TAIL
+#endif
+#define WL_LBQ(LBM, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, TAIL)                                         \
+    LBM("v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, TAIL)
+
+#define WALK_ASM(LBM)                                                                                    \
+    asm volatile(                                                                                                     \
+        /* prologue: block c's entries, block c + 1's header, LB0's offsets / events */                               \
+        "v_mov_b32 %[lh], %[sn]\n\t"                                                                                  \
+        "v_add_u32 %[ln], %[sn], %[l16]\n\t"                                                                          \
+        "ds_read_b128 v[100:103], %[la]\n\t"                                                                          \
+        "ds_read_b128 v[104:107], %[la] offset:8192\n\t"                                                              \
+        "ds_read_b128 v[108:111], %[la] offset:1024\n\t"                                                              \
+        "ds_read_b128 v[112:115], %[la] offset:9216\n\t"                                                              \
+        "ds_read_b128 v[116:119], %[la] offset:2048\n\t"                                                              \
+        "ds_read_b128 v[120:123], %[la] offset:10240\n\t"                                                             \
+        "ds_read_b128 v[124:127], %[la] offset:3072\n\t"                                                              \
+        "ds_read_b128 v[128:131], %[la] offset:11264\n\t"                                                             \
+        "ds_read_b128 v[132:135], %[la] offset:4096\n\t"                                                              \
+        "ds_read_b128 v[136:139], %[la] offset:12288\n\t"                                                             \
+        "ds_read_b128 v[140:143], %[la] offset:5120\n\t"                                                              \
+        "ds_read_b128 v[144:147], %[la] offset:13312\n\t"                                                             \
+        "ds_read_b128 v[148:151], %[la] offset:6144\n\t"                                                              \
+        "ds_read_b128 v[152:155], %[la] offset:14336\n\t"                                                             \
+        "ds_read_b128 v[156:159], %[la] offset:7168\n\t"                                                              \
+        "ds_read_b128 v[160:163], %[la] offset:15360\n\t"                                                             \
+        "ds_read_b32 v164, %[lh] offset:16384\n\t"                                                                    \
+        "s_lshl_b32 %[s4], %[S], 2\n\t"                                                                               \
+        "s_mov_b32 %[kb0], %[kb]\n\t"                                                                                 \
+        "s_mov_b32 %[d0], %[d]\n\t"                                                                                   \
+        "s_mov_b32 %[nrep0], %[nrep]\n\t"                                                                             \
+        "v_mov_b32 %[acc], 0\n\t"                                                                                     \
+        "s_waitcnt lgkmcnt(0)\n\t"                                                                                    \
+        "v_mul_lo_u32 %[t], %[d], v102\n\t"                                                                           \
+        "v_add3_u32 %[xa], v100, %[kb], %[t]\n\t"                                                                     \
+        "v_cmp_gt_u32_e32 vcc, %[xa], v101\n"                                                                         \
+        "9:\n\t"                                                                                                      \
+        WL_LBQ(LBM, 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]",                               \
+               WL_PF(100:103, 104:107, 0, 8192))                                                                      \
+        WL_LBQ(LBM, 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]",                               \
+               WL_PF(108:111, 112:115, 1024, 9216))                                                                   \
+        WL_LBQ(LBM, 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]",                               \
+               WL_PF(116:119, 120:123, 2048, 10240))                                                                  \
+        WL_LBQ(LBM, 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]",                               \
+               WL_PF(124:127, 128:131, 3072, 11264))                                                                  \
+        WL_LBQ(LBM, 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]",                               \
+               WL_PF(132:135, 136:139, 4096, 12288))                                                                  \
+        WL_LBQ(LBM, 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]",                               \
+               WL_PF(140:143, 144:147, 5120, 13312))                                                                  \
+        WL_LBQ(LBM, 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]",                               \
+               WL_PF(148:151, 152:155, 6144, 14336))                                                                  \
+        /* lane-block 7: its N0 is the next block's lane-block 0 (read after LB 0; the */                             \
+        /* header of block c + 1 was the first read of this block) */                                                 \
+        "s_waitcnt lgkmcnt(13)\n\t"                                                                                   \
+        "v_readfirstlane_b32 %[snx], v164\n\t"                                                                        \
+        "s_sub_u32 %[dS], %[snx], %[S]\n\t"                                                                           \
+        "v_add_u32 %[sx7], %[dS], v102\n\t"                                                                           \
+        LBM("v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v100", "v101", "%[sx7]", "%[xb]",      \
+              "%[xa]", "")                                                                                            \
+        /* block end */                                                                                               \
+        "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"                                                                      \
+        "s_mul_i32 %[tS], %[dS], %[d]\n\t"                                                                            \
+        "s_cmp_lg_u64 %[bad], 0\n\t"                                                                                  \
+        "s_cbranch_scc1 8f\n\t"                                                                                       \
+        "v_mov_b32 %[s7], v158\n\t"                                                                                   \
+        WL_PF(156:159, 160:163, 7168, 15360)                                                                          \
+        "s_add_u32 %[kb], %[kb], %[tS]\n\t"                                                                           \
+        "s_mov_b32 %[Sp], %[S]\n\t"                                                                                   \
+        "s_mov_b32 %[S], %[snx]\n\t"                                                                                  \
+        "s_lshl_b32 %[s4], %[S], 2\n\t"                                                                               \
+        "s_mov_b32 %[kb0], %[kb]\n\t"                                                                                 \
+        "s_mov_b32 %[d0], %[d]\n\t"                                                                                   \
+        "s_mov_b32 %[nrep0], %[nrep]\n\t"                                                                             \
+        "v_mov_b32 %[acc], 0\n\t"                                                                                     \
+        "s_add_u32 %[c], %[c], 1\n\t"                                                                                 \
+        "s_add_u32 %[sn], %[sn], %[slot]\n\t"                                                                         \
+        "s_cmp_eq_u32 %[sn], %[rend]\n\t"                                                                             \
+        "s_cselect_b32 %[sn], %[ring], %[sn]\n\t"                                                                     \
+        "s_waitcnt lgkmcnt(0)\n\t"                                                                                    \
+        "s_barrier\n\t"                                                                                               \
+        "v_mov_b32 %[lh], %[sn]\n\t"                                                                                  \
+        "v_add_u32 %[ln], %[sn], %[l16]\n\t"                                                                          \
+        "ds_read_b32 v164, %[lh] offset:16384\n\t"                                                                    \
+        "s_cmp_lt_u32 %[c], %[nblk]\n\t"                                                                              \
+        "s_cbranch_scc1 9b\n"                                                                                         \
+        "8:\n\t"                                                                                                      \
+        "s_waitcnt lgkmcnt(0)"                                                                                        \
+        : [xa] "=&v"(xa), [xb] "=&v"(xb), [t] "=&v"(t), [off] "=&v"(off), [acc] "=&v"(acc),                           \
+          [sx7] "=&v"(sx7), [ln] "=&v"(ln), [lh] "=&v"(lh), [s7] "+v"(s7),                                            \
+          [pm] "=&s"(pm), [bad] "=&s"(bad),                                                                           \
+          [kb] "+s"(kb), [d] "+s"(d), [nrep] "+s"(nrep), [c] "+s"(c), [S] "+s"(S), [Sp] "+s"(Sprev),                  \
+          [kb0] "=&s"(kb0), [d0] "=&s"(d0), [nrep0] "=&s"(nrep0), [sn] "+s"(sn),                                      \
+          [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr), [snx] "=&s"(snx), [dS] "=&s"(dS),         \
+          [tS] "=&s"(tS), [s4] "=&s"(s4)                                                                              \
+        : [la] "v"(la), [l16] "v"(lane16), [nblk] "s"(nblk), [ring] "s"(ring), [rend] "s"(rend), [slot] "s"(kSlot),   \
+          [yb] "s"(y)                                                                                                 \
+        : "scc", "vcc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",\
+          "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",     \
+          "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135",     \
+          "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148",     \
+          "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161",     \
+          "v162", "v163", "v164");
 
 struct WalkLoop {
     uint32_t c, kb, d, nrep;          // block index; offset model; live repair count
@@ -1351,7 +1482,9 @@ struct WalkLoop {
 };
 
 // Runs blocks c .. nblk - 1 until one fails its interval test (returns with c = that
-// block, not yet barriered) or all are done (c = nblk).
+// block, not yet barriered) or all are done (c = nblk).  PV: 0 the product, 1 / 2 the
+// tuning build's timing variants (WL_LB_NOREP / WL_LB_NOST).
+template <int PV>
 __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32_t ring, float* y, uint32_t lane16)
 {
     constexpr uint32_t kSlot = (uint32_t)sizeof(WalkBufE);
@@ -1363,102 +1496,16 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
     uint32_t j, dk1, dk2, nr, snx, dS, tS, s4;
     unsigned long long pm, bad;
     uint32_t kb = w.kb, d = w.d, nrep = w.nrep, c = w.c, S = w.S, Sprev = w.Sprev, kb0, d0, nrep0;
-    asm volatile(
-        // prologue: block c's entries, block c + 1's header, LB0's offsets / events
-        "v_mov_b32 %[lh], %[sn]\n\t"
-        "v_add_u32 %[ln], %[sn], %[l16]\n\t"
-        "ds_read_b128 v[100:103], %[la]\n\t"
-        "ds_read_b128 v[104:107], %[la] offset:8192\n\t"
-        "ds_read_b128 v[108:111], %[la] offset:1024\n\t"
-        "ds_read_b128 v[112:115], %[la] offset:9216\n\t"
-        "ds_read_b128 v[116:119], %[la] offset:2048\n\t"
-        "ds_read_b128 v[120:123], %[la] offset:10240\n\t"
-        "ds_read_b128 v[124:127], %[la] offset:3072\n\t"
-        "ds_read_b128 v[128:131], %[la] offset:11264\n\t"
-        "ds_read_b128 v[132:135], %[la] offset:4096\n\t"
-        "ds_read_b128 v[136:139], %[la] offset:12288\n\t"
-        "ds_read_b128 v[140:143], %[la] offset:5120\n\t"
-        "ds_read_b128 v[144:147], %[la] offset:13312\n\t"
-        "ds_read_b128 v[148:151], %[la] offset:6144\n\t"
-        "ds_read_b128 v[152:155], %[la] offset:14336\n\t"
-        "ds_read_b128 v[156:159], %[la] offset:7168\n\t"
-        "ds_read_b128 v[160:163], %[la] offset:15360\n\t"
-        "ds_read_b32 v164, %[lh] offset:16384\n\t"
-        "s_lshl_b32 %[s4], %[S], 2\n\t"
-        "s_mov_b32 %[kb0], %[kb]\n\t"
-        "s_mov_b32 %[d0], %[d]\n\t"
-        "s_mov_b32 %[nrep0], %[nrep]\n\t"
-        "v_mov_b32 %[acc], 0\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_mul_lo_u32 %[t], %[d], v102\n\t"
-        "v_add3_u32 %[xa], v100, %[kb], %[t]\n\t"
-        "v_cmp_gt_u32_e32 vcc, %[xa], v101\n"
-        "9:\n\t"
-        WL_LBQ(100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]",
-               WL_PF(100:103, 104:107, 0, 8192))
-        WL_LBQ(108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]",
-               WL_PF(108:111, 112:115, 1024, 9216))
-        WL_LBQ(116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]",
-               WL_PF(116:119, 120:123, 2048, 10240))
-        WL_LBQ(124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]",
-               WL_PF(124:127, 128:131, 3072, 11264))
-        WL_LBQ(132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]",
-               WL_PF(132:135, 136:139, 4096, 12288))
-        WL_LBQ(140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]",
-               WL_PF(140:143, 144:147, 5120, 13312))
-        WL_LBQ(148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]",
-               WL_PF(148:151, 152:155, 6144, 14336))
-        // lane-block 7: its N0 is the next block's lane-block 0 (read after LB 0; the
-        // header of block c + 1 was the first read of this block)
-        "s_waitcnt lgkmcnt(13)\n\t"
-        "v_readfirstlane_b32 %[snx], v164\n\t"
-        "s_sub_u32 %[dS], %[snx], %[S]\n\t"
-        "v_add_u32 %[sx7], %[dS], v102\n\t"
-        WL_LB("v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v100", "v101", "%[sx7]", "%[xb]",
-              "%[xa]", "")
-        // block end
-        "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"
-        "s_mul_i32 %[tS], %[dS], %[d]\n\t"
-        "s_cmp_lg_u64 %[bad], 0\n\t"
-        "s_cbranch_scc1 8f\n\t"
-        "v_mov_b32 %[s7], v158\n\t"
-        WL_PF(156:159, 160:163, 7168, 15360)
-        "s_add_u32 %[kb], %[kb], %[tS]\n\t"
-        "s_mov_b32 %[Sp], %[S]\n\t"
-        "s_mov_b32 %[S], %[snx]\n\t"
-        "s_lshl_b32 %[s4], %[S], 2\n\t"
-        "s_mov_b32 %[kb0], %[kb]\n\t"
-        "s_mov_b32 %[d0], %[d]\n\t"
-        "s_mov_b32 %[nrep0], %[nrep]\n\t"
-        "v_mov_b32 %[acc], 0\n\t"
-        "s_add_u32 %[c], %[c], 1\n\t"
-        "s_add_u32 %[sn], %[sn], %[slot]\n\t"
-        "s_cmp_eq_u32 %[sn], %[rend]\n\t"
-        "s_cselect_b32 %[sn], %[ring], %[sn]\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_barrier\n\t"
-        "v_mov_b32 %[lh], %[sn]\n\t"
-        "v_add_u32 %[ln], %[sn], %[l16]\n\t"
-        "ds_read_b32 v164, %[lh] offset:16384\n\t"
-        "s_cmp_lt_u32 %[c], %[nblk]\n\t"
-        "s_cbranch_scc1 9b\n"
-        "8:\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : [xa] "=&v"(xa), [xb] "=&v"(xb), [t] "=&v"(t), [off] "=&v"(off), [acc] "=&v"(acc),
-          [sx7] "=&v"(sx7), [ln] "=&v"(ln), [lh] "=&v"(lh), [s7] "+v"(s7),
-          [pm] "=&s"(pm), [bad] "=&s"(bad),
-          [kb] "+s"(kb), [d] "+s"(d), [nrep] "+s"(nrep), [c] "+s"(c), [S] "+s"(S), [Sp] "+s"(Sprev),
-          [kb0] "=&s"(kb0), [d0] "=&s"(d0), [nrep0] "=&s"(nrep0), [sn] "+s"(sn),
-          [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr), [snx] "=&s"(snx), [dS] "=&s"(dS),
-          [tS] "=&s"(tS), [s4] "=&s"(s4)
-        : [la] "v"(la), [l16] "v"(lane16), [nblk] "s"(nblk), [ring] "s"(ring), [rend] "s"(rend), [slot] "s"(kSlot),
-          [yb] "s"(y)
-        : "scc", "vcc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
-          "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
-          "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135",
-          "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148",
-          "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161",
-          "v162", "v163", "v164");
+    if constexpr (PV == 0) {
+        WALK_ASM(WL_LB);
+    }
+#ifdef LDSP_TUNING
+    else if constexpr (PV == 1) {
+        WALK_ASM(WL_LB_NOREP);
+    } else {
+        WALK_ASM(WL_LB_NOST);
+    }
+#endif
     w.c = c;
     w.kb = kb;
     w.d = d;
@@ -1522,7 +1569,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     PrevLB prev{0u, 1, 0u, true};
     unsigned long long cyc_walk = 0, cyc_wait = 0;
     unsigned long long clk_walk = 0, clk_wait = 0;          // VAR & 8 (tuning): shader clocks
-    if constexpr (F24 && !STATS && VAR == 0) {
+    if constexpr (F24 && !STATS && (VAR == 0 || VAR >= 32)) {
         // the product path: the block loop in one asm statement (walk_asm_loop)
         if (wave != 0) {
             for (long c = 0; c < nblk; c++) {
@@ -1542,7 +1589,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 const uint32_t Sn = rfl(buf[c0 % kRing].hdr[0]);
                 w.kb += (Sn - w.S) * w.d;
                 w.S = Sn;
-                walk_asm_loop(w, (uint32_t)nblk, ring, y, (uint32_t)lane * 16u);
+                walk_asm_loop<VAR / 32>(w, (uint32_t)nblk, ring, y, (uint32_t)lane * 16u);
                 if (w.c > c0) prev = PrevLB{w.s7, 64, w.Sprev, false};
                 if (w.c >= (uint32_t)nblk) break;
                 // block c failed its interval test: undo its speculative stores (the
@@ -1584,7 +1631,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             S = w.S;
         }
     }
-    for (long c = 0; c < ((F24 && !STATS && VAR == 0) ? 0 : nblk); c++) {
+    for (long c = 0; c < ((F24 && !STATS && (VAR == 0 || VAR >= 32)) ? 0 : nblk); c++) {
         const unsigned long long t0 = STATS ? wall_clock64() : 0;
         const unsigned long long c0 = (VAR & 8) ? __builtin_amdgcn_s_memtime() : 0;
         if (wave != 0) {
@@ -1901,7 +1948,7 @@ void pll_back(const PllCall& c, hipStream_t s)
                 switch (var) {
                 WALK_VAR(1) WALK_VAR(2) WALK_VAR(3) WALK_VAR(4) WALK_VAR(5) WALK_VAR(6) WALK_VAR(7)
                 WALK_VAR(8) WALK_VAR(9) WALK_VAR(10) WALK_VAR(11) WALK_VAR(12) WALK_VAR(13) WALK_VAR(14) WALK_VAR(15)
-                WALK_VAR(16) WALK_VAR(24)
+                WALK_VAR(16) WALK_VAR(24) WALK_VAR(32) WALK_VAR(64)
                 default: break;
                 }
 #undef WALK_VAR

@@ -145,6 +145,26 @@ struct IirModalPlan {
     int variant = 0;      // tuning builds only (timing experiments, wrong outputs): bit 0 no look-back,
                           // bit 1 no pass 2, bit 2 no pass 1 / scan
 };
+// IIR -> resampler fusion (liquiddsp.filter_resample, k_iir_modal<RS>): each unit's
+// filter outputs stay in LDS and feed the resampler outputs whose sub_len-sample
+// window lies inside the unit (the resampler's own arithmetic, resamp_dev.hpp);
+// the unit's first and last H = sub_len - 1 outputs go to `side`, from which
+// k_iir_resamp_edges computes the outputs whose window straddles a unit boundary
+// (and the resampler's new history).  The filter outputs never reach HBM.
+struct IirResampFuse {
+    const float* sub;     // [npfb][sub_len] branch taps, reversed (ResampObj::sub; complex interleaved if ctaps)
+    uint64_t P0;          // the resampler's phase at the call's start
+    uint32_t step;
+    int bits_index, sub_len;
+    int ctaps;            // complex taps (resamp_cccf, the ComplexResampler): rs_mac over both components
+    long K;               // outputs of the call
+    float* side;          // [units][2][H][ncomp]: head (first H) and tail (last H, right-aligned) outputs
+    float* y;             // resampler outputs ([K][ncomp] floats)
+};
+size_t iir_resamp_side_bytes(size_t n, int sub_len, bool cplx);
+void iir_modal_resamp(bool cplx, const IirModalCoef& cf, const void* x, size_t n, const double* st_in,
+                      double* st_out, const IirModalPlan& p, const IirResampFuse& f, const void* hist,
+                      void* hist_out, hipStream_t s);
 long iir_modal_units(size_t n);   // workgroups (2048-sample look-back units) of a call
 void iir_modal(bool cplx, const IirModalCoef& cf, const void* x, size_t n, const double* st_in, double* st_out,
                const IirModalPlan& p, void* y, hipStream_t s, bool iq16 = false);

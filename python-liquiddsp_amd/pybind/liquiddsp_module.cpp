@@ -978,6 +978,31 @@ const char* kAgcDoc = "Automatic gain control with squelch for complex IQ (liqui
 
 } // namespace
 
+// the registered IIR / resampler classes as their common bases (filter_resample)
+template <typename... T>
+IIR* iir_of(const py::object& o)
+{
+    IIR* r = nullptr;
+    ((r = (!r && py::isinstance<T>(o)) ? static_cast<IIR*>(&o.cast<T&>()) : r), ...);
+    return r;
+}
+IIR& as_iir(const py::object& o)
+{
+    IIR* r = iir_of<ComplexIIRFilter, RealIIRFilter, CIIRFilter, RIIRFilter, PassIIR<0, true>, PassIIR<1, true>,
+                    BandXIIR<2, true>, BandXIIR<3, true>, PassIIR<0, false>, PassIIR<1, false>, BandXIIR<2, false>,
+                    BandXIIR<3, false>, DeemphasisFilter>(o);
+    if (!r) throw py::type_error("filter_resample: iir must be one of the IIR filter classes");
+    return *r;
+}
+Resampler& as_resampler(const py::object& o)
+{
+    if (py::isinstance<ComplexResampler>(o)) return o.cast<ComplexResampler&>();
+    if (py::isinstance<RealResampler>(o)) return o.cast<RealResampler&>();
+    if (py::isinstance<CResampler>(o)) return o.cast<CResampler&>();
+    if (py::isinstance<RResampler>(o)) return o.cast<RResampler&>();
+    throw py::type_error("filter_resample: resampler must be one of the resampler classes");
+}
+
 PYBIND11_MODULE(_liquiddsp, m)
 {
     m.doc() = "MI355X-native replacement for python-liquiddsp's streaming DSP classes (libldsp C ABI)";
@@ -1096,6 +1121,44 @@ PYBIND11_MODULE(_liquiddsp, m)
         },
         py::arg("nco"), py::arg("fir"), py::arg("x"),
         "fir(nco.mix_up(x)) in one pass: same output bits and state updates as the two calls");
+
+    // ---- IIR fused into the resampler (README chain's first two stages; opt-in, not in wrapper.cpp)
+    m.def(
+        "filter_resample",
+        [](py::object iir_o, py::object rs_o, const py::handle& x) {
+            IIR& iir = as_iir(iir_o);
+            Resampler& rs = as_resampler(rs_o);
+            const bool c = rs.cplx;
+            if (iir.cplx != c) throw py::value_error("filter_resample: the filter and the resampler must both be complex or both real");
+            if (is_device_tensor(x)) {
+                DevIn d = dev_in(x, c);
+                size_t nout = 0;
+                check(ldsp_resamp_num_outputs(rs.q, d.n, &nout));
+                py::object out = dev_empty(nout, c, d.device);
+                size_t nw = 0;
+                check(ldsp_iirfilt_resamp_execute(iir.q, rs.q, d.ptr, d.n, tptr(out), nout, &nw, LDSP_MEM_DEVICE, d.stream));
+                return out;
+            }
+            py::array a = c ? py::array(carr::ensure(x)) : py::array(farr::ensure(x));
+            if (!a) throw py::error_already_set();
+            const size_t n = (size_t)a.size();
+            size_t nout = 0;
+            check(ldsp_resamp_num_outputs(rs.q, n, &nout));
+            py::array out = c ? py::array(py::array_t<cf>(nout)) : py::array(py::array_t<float>(nout));
+            void* yp = out.mutable_data();
+            const void* xp = a.data();
+            size_t nw = 0;
+            int rc;
+            {
+                py::gil_scoped_release rel;
+                rc = ldsp_iirfilt_resamp_execute(iir.q, rs.q, xp, n, yp, nout, &nw, LDSP_MEM_HOST, nullptr);
+            }
+            check(rc);
+            return py::object(out);
+        },
+        py::arg("iir"), py::arg("resampler"), py::arg("x"),
+        "resampler(iir(x)) in one pass (the filter's outputs stay on chip when it takes the fast modal scan): "
+        "same output bits and state updates as the two calls");
 
     // ---- bytes_to_iq, Delay (wrapper.cpp:13, 25-28)
     m.def("bytes_to_iq", &bytes_to_iq, py::arg("byts"));

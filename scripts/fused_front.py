@@ -1,0 +1,39 @@
+"""IIR -> resampler fusion (liquiddsp.filter_resample) at the bench size: per-kernel
+HIP-event times of the fused front against the two calls on 64 Mi samples, and
+the multi-channel component (8 AMRadio chains on one GPU) with and without it."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.environ.get("LDSP_PKG_DIR", os.path.join(REPO, "python-liquiddsp_amd"))]
+import bench  # noqa: E402  (sets GPU_MAX_HW_QUEUES before torch initialises HIP)
+import torch  # noqa: E402
+import liquiddsp as L  # noqa: E402
+
+dev = torch.device("cuda", 0)
+n = 64 << 20
+x = bench.synth_channel(n, 0, dev)
+
+
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    L._profile_reset()
+    L._profile_enable(True)
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    L._profile_enable(False)
+    return {k: round(v[1] / v[0], 4) for k, v in L._profile_report().items()}
+
+
+r1, r2 = bench.AMRadio(L), bench.AMRadio(L)
+out = {"two_calls": timed(lambda: r1.resample(r1.bandpass(x))),
+       "fused": timed(lambda: L.filter_resample(r2.bandpass, r2.resample, x))}
+for k in ("two_calls", "fused"):
+    out[k + "_ms"] = round(sum(out[k].values()), 4)
+print(json.dumps(out), flush=True)
+del x
+for fused in (True, False):
+    print(json.dumps(bench.multi_channel(L, dev, fused=fused)), flush=True)

@@ -141,6 +141,25 @@ __global__ void __launch_bounds__(64) k_loop(const uint4* E, uint32_t* out, int 
             acc += x;
             x = e.x;             // every lane an event again in the next lane-block
             continue;
+        } else if (V == 11) {    // exec = the events (v_cmpx): lane j's values by readfirstlane,
+            // off the s_ff1; exec = the lanes above j (s_ff1 exec, s_lshl) for the update
+            uint32_t j, dk1, dk2;
+#define WF_BODY \
+    "v_readfirstlane_b32 %[dk1], %[e1x]\n\t" \
+    "v_readfirstlane_b32 %[dk2], %[e1y]\n\t" \
+    "s_ff1_i32_b64 %[j], exec\n\t" \
+    "s_lshl_b64 exec, -2, %[j]\n\t" \
+    "v_mad_i32_i24 %[x], %[sx], %[dk1], %[x]\n\t" \
+    "v_add_u32 %[x], %[dk2], %[x]\n\t" \
+    "s_add_u32 %[kb], %[kb], %[dk2]\n\t" \
+    "s_add_u32 %[d], %[d], %[dk1]\n\t" \
+    "v_cmpx_gt_u32_e32 vcc, %[x], %[w]\n\t"
+            asm volatile("v_add_u32 %[x], %[b], %[x]\n\tv_cmpx_gt_u32_e32 vcc, %[x], %[w]\n\t"
+                         "s_cbranch_execz 2f\n1:\n\t" WF_BODY "s_cbranch_execz 2f\n\t" WF_BODY "s_cbranch_execz 2f\n\t"
+                         WF_BODY "s_cbranch_execz 2f\n\t" WF_BODY "s_cbranch_execnz 1b\n2:\n\ts_mov_b64 exec, -1" WX_OPS);
+            acc += x;
+            x = e.x;
+            continue;
         } else if (V == 3) {     // pure SALU loop over the mask (no ballot per step)
             do {
                 const int j = __builtin_ctzll(mask);
@@ -186,6 +205,13 @@ int main()
     run(k_loop<8>, "V8 production asm, unrolled x4");
     run(k_loop<9>, "V9 exec-masked, VCC branch, rolled");
     run(k_loop<10>, "V10 exec-masked, VCC branch, unrolled x4");
+    uint32_t o10[64], o11[64];
+    hipMemcpy(o10, dout, 256, hipMemcpyDeviceToHost);
+    run(k_loop<11>, "V11 v_cmpx + readfirstlane, unrolled x4");
+    hipMemcpy(o11, dout, 256, hipMemcpyDeviceToHost);
+    int same = 1;
+    for (int i = 0; i < 64; i++) same &= o10[i] == o11[i];
+    printf("V11 results %s V10's\n", same ? "equal" : "DIFFER FROM");
     // s_memtime frequency: compare against wall clock
     hipEvent_t a, b;
     hipEventCreate(&a);

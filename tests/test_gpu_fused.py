@@ -152,3 +152,61 @@ def test_mix_filter_config3_full_size_vs_oracle(ld, ora):
     on.state = ((a * dtheta) & 0xFFFFFFFF, dtheta)
     ref = ora.FIRFilter(h, cplx=True)(on.mix_down(xd[a:].cpu().numpy()))[L - 1:]
     assert maxrel(y[n - w:].cpu().numpy(), ref) <= 1e-6
+
+
+# ------------------------------------------------------------------ IIR -> resampler
+def _iir_rs(ld, cplx, exact=False, fc=15000 / 2e6, rate=48000 / 2e6):
+    if cplx:
+        f = ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=fc)
+        r = ld.ComplexResampler(rate=rate, Fc=rate)
+    else:
+        f = ld.RealIIRFilter(filter_type="cheby2", order=8, Fc=fc)
+        r = ld.RealResampler(rate=rate, Fc=rate)
+    f.exact = exact
+    return f, r
+
+
+@pytest.mark.parametrize("cplx", [True, False])
+@pytest.mark.parametrize("exact", [False, True])
+def test_filter_resample_equals_two_calls(ld, rng, cplx, exact):
+    """liquiddsp.filter_resample(iir, resampler, x) == resampler(iir(x)) bit for
+    bit on ragged device calls (a unit boundary's window from the side buffer, the
+    call's first window from the resampler history, calls shorter than the
+    window), and both objects continue the same streams afterwards (IIR state,
+    resampler phase and history).  exact: the two-call fallback."""
+    import torch
+    n = (1 << 20) + 12_345
+    x = cgauss(rng, n) if cplx else rng.standard_normal(n).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    cuts = [0, 1, 30, 2048, 2048 + 39, 4096 + 40, 70_001, 600_000, n]
+    fa, ra = _iir_rs(ld, cplx, exact)
+    fb, rb = _iir_rs(ld, cplx, exact)
+    ys, refs = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        ys.append(ld.filter_resample(fa, ra, xd[a:b]))
+        refs.append(rb(fb(xd[a:b])))
+    y, ref = torch.cat(ys).cpu().numpy(), torch.cat(refs).cpu().numpy()
+    assert y.shape == ref.shape and y.size > 0.023 * n
+    eq = bits(y) == bits(ref)
+    assert eq.all(), f"{(~eq).sum()} of {eq.size} differ; first at {int(np.argmin(eq))}"
+    x2 = torch.from_numpy(cgauss(rng, 50_000) if cplx else rng.standard_normal(50_000).astype(np.float32)).cuda()
+    assert torch.equal(ra(fa(x2)).view(torch.int32), rb(fb(x2)).view(torch.int32))
+
+
+def test_filter_resample_64Mi_and_host(ld, rng):
+    """The bench chain's front at the BASELINE size (64 Mi in one call) and the
+    numpy path: the same bits as the two calls."""
+    import torch
+    import bench
+    n = 64 << 20
+    xd = bench.synth_channel(n, 0, torch.device("cuda", 0))
+    fa, ra = _iir_rs(ld, True)
+    fb, rb = _iir_rs(ld, True)
+    y = ld.filter_resample(fa, ra, xd)
+    ref = rb(fb(xd))
+    assert y.shape == ref.shape and y.numel() > 1_600_000
+    assert torch.equal(y.view(torch.int32), ref.view(torch.int32))
+    xh = xd[:300_001].cpu().numpy()
+    yh = ld.filter_resample(fa, ra, xh)
+    assert isinstance(yh, np.ndarray)
+    assert np.array_equal(bits(yh), bits(rb(fb(xh))))
