@@ -448,6 +448,15 @@ struct IirObj {
 
     int fsz() const { return sos ? 3 * (int)nsos : nv; }
     int ncomp() const { return cplx ? 2 : 1; }
+    // Long look-backs: outside its one-XCD small-call mode (<= 16 J units) the
+    // modal scan's 8 per-XCD unit ranges each start with J(J+1)/2 predecessor
+    // recomputes (k_iir_modal.hip); a slowly decaying filter (J >= 16) whose
+    // recomputes would exceed a quarter of the call's units takes the blocked scan.
+    bool modal_pays(size_t n) const
+    {
+        const long units = k::iir_modal_units(n), J = mf.J;
+        return J < 16 || units <= 16 * J || 4 * J * (J + 1) <= units / 4;
+    }
     // which kernel path a call of n samples takes
     enum Path { kSpec, kSeq, kModal, kBlk, kScan };
     Path path_for(size_t n) const
@@ -458,7 +467,7 @@ struct IirObj {
         if (D == 0) return kSeq;
         if (path_force == 0 && spec_W > 0 && spec_W <= 16384 && (long)n >= spec_min) return kSpec;
         if (mode == LDSP_MODE_EXACT) return kSeq;
-        if (mf.ok && path_force != 1) return kModal;
+        if (mf.ok && path_force != 1 && (path_force >= 2 || modal_pays(n))) return kModal;
         return D <= k::kIirBlkMaxD ? kBlk : kScan;
     }
 

@@ -1372,6 +1372,28 @@ __device__ __forceinline__ bool walk_blk8_sel(uint32_t lds, float* yb, uint32_t&
     "v_mul_lo_u32 %[t], %[d], " SXN "\n\t"                                                                 \
     "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
     "v_cmp_gt_u32_e32 vcc, " XN ", " N0Y "\n\t" TAIL
+// HELPER: the walker's side of a design where other waves store the repaired
+// outputs and count the repairs: the repaired lanes' test via a select (no exec
+// switch), the offsets written to LDS for the helpers (timing only: one junk slot)
+#define WL_LB_HELPER(E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, SXN, X, XN, TAIL)                    \
+    "s_cbranch_vccz 2f\n"                                                                                  \
+    "1:\n\t"                                                                                               \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccnz 1b\n"                                                    \
+    "3:\n\t"                                                                                               \
+    "s_mov_b64 exec, -1\n"                                                                                 \
+    "2:\n\t"                                                                                               \
+    "v_mul_lo_u32 %[t], %[d], " SXN "\n\t"                                                                 \
+    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
+    "v_cmp_gt_u32_e64 %[pm], " X ", " E0Y "\n\t"                                                           \
+    "v_sub_u32 %[t], " X ", " E0W "\n\t"                                                                   \
+    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
+    "v_cmp_gt_u32_e32 vcc, " XN ", " N0Y "\n\t"                                                            \
+    "v_cndmask_b32_e64 %[t], 0, %[t], %[pm]\n\t"                                                           \
+    "v_or_b32 %[acc], %[acc], %[t]\n\t"                                                                    \
+    "ds_write_b32 %[xs], " X "\n\t" TAIL
 #endif
 #define WL_LBQ(LBM, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, TAIL)                                         \
     LBM("v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, TAIL)
@@ -1465,7 +1487,8 @@ __device__ __forceinline__ bool walk_blk8_sel(uint32_t lds, float* yb, uint32_t&
           [kb0] "=&s"(kb0), [d0] "=&s"(d0), [nrep0] "=&s"(nrep0), [sn] "+s"(sn),                                      \
           [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr), [snx] "=&s"(snx), [dS] "=&s"(dS),         \
           [tS] "=&s"(tS), [s4] "=&s"(s4)                                                                              \
-        : [la] "v"(la), [l16] "v"(lane16), [nblk] "s"(nblk), [ring] "s"(ring), [rend] "s"(rend), [slot] "s"(kSlot),   \
+        : [la] "v"(la), [l16] "v"(lane16), [nblk] "s"(nblk), [ring] "s"(ring), [rend] "s"(rend), [slot] "s"(kSlot), \
+          [xs] "v"(xs),   \
           [yb] "s"(y)                                                                                                 \
         : "scc", "vcc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",\
           "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",     \
@@ -1485,7 +1508,8 @@ struct WalkLoop {
 // block, not yet barriered) or all are done (c = nblk).  PV: 0 the product, 1 / 2 the
 // tuning build's timing variants (WL_LB_NOREP / WL_LB_NOST).
 template <int PV>
-__device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32_t ring, float* y, uint32_t lane16)
+__device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32_t ring, float* y, uint32_t lane16,
+                                              uint32_t xs = 0)
 {
     constexpr uint32_t kSlot = (uint32_t)sizeof(WalkBufE);
     static_assert(sizeof(WalkBufE) == 16400, "slot stride below");
@@ -1502,8 +1526,10 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
 #ifdef LDSP_TUNING
     else if constexpr (PV == 1) {
         WALK_ASM(WL_LB_NOREP);
-    } else {
+    } else if constexpr (PV == 2) {
         WALK_ASM(WL_LB_NOST);
+    } else {
+        WALK_ASM(WL_LB_HELPER);
     }
 #endif
     w.c = c;
@@ -1527,6 +1553,9 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     LDSP_LATENCY_CRITICAL();
     __shared__ WalkBufE buf[kRing];      // ring: block c in buf[c % kRing], DMA'd kRing - 1 blocks ahead
     __shared__ float wtab[1024];         // NCO table for the fallback's full loop steps
+#ifdef LDSP_TUNING
+    __shared__ uint32_t xscratch[64];    // timing variant 96 (WL_LB_HELPER) writes its offsets here
+#endif
     // Own the CU: 8 waves x 256 VGPRs fill every SIMD's register file, so no wave of
     // the kernels running beside the walk (the next call's AGC, candidates, ...)
     // is placed on the walker's SIMD and takes issue slots from its serial chain.
@@ -1589,7 +1618,12 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 const uint32_t Sn = rfl(buf[c0 % kRing].hdr[0]);
                 w.kb += (Sn - w.S) * w.d;
                 w.S = Sn;
+#ifdef LDSP_TUNING
+                walk_asm_loop<VAR / 32>(w, (uint32_t)nblk, ring, y, (uint32_t)lane * 16u,
+                                        (uint32_t)(uintptr_t)&xscratch[lane]);
+#else
                 walk_asm_loop<VAR / 32>(w, (uint32_t)nblk, ring, y, (uint32_t)lane * 16u);
+#endif
                 if (w.c > c0) prev = PrevLB{w.s7, 64, w.Sprev, false};
                 if (w.c >= (uint32_t)nblk) break;
                 // block c failed its interval test: undo its speculative stores (the
@@ -1948,7 +1982,7 @@ void pll_back(const PllCall& c, hipStream_t s)
                 switch (var) {
                 WALK_VAR(1) WALK_VAR(2) WALK_VAR(3) WALK_VAR(4) WALK_VAR(5) WALK_VAR(6) WALK_VAR(7)
                 WALK_VAR(8) WALK_VAR(9) WALK_VAR(10) WALK_VAR(11) WALK_VAR(12) WALK_VAR(13) WALK_VAR(14) WALK_VAR(15)
-                WALK_VAR(16) WALK_VAR(24) WALK_VAR(32) WALK_VAR(64)
+                WALK_VAR(16) WALK_VAR(24) WALK_VAR(32) WALK_VAR(64) WALK_VAR(96)
                 default: break;
                 }
 #undef WALK_VAR

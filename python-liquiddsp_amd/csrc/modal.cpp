@@ -17,6 +17,7 @@
 #include "modal.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 
 namespace ldsp {
@@ -361,13 +362,64 @@ ModalForm modal_form(int D, const std::vector<ld>& A, const std::vector<ld>& B, 
     f.err = err;
     if (!(err <= 1e-10)) return fail("modal form ill-conditioned");
 
-    // look-back depth: max |lambda|^(2048 J) < 2^-70
+    // look-back depth.  A unit's start state drops the end states of the units
+    // J and more before it, i.e. sum_{i >= J} A^(2048 i) BL; bound that tail with
+    // the norms of the actual 2 x 2 section powers (a section's powers can grow
+    // ~1/sin(theta) above |lambda|^k before they decay) times the modal basis's
+    // conditioning ||to_v|| ||from_v|| (the look-back runs in modal coordinates),
+    // and take the smallest J whose bound is below 2^-70.  Start from the
+    // spectral-radius estimate max |lambda|^(2048 J) < 2^-70.
     int J = 1;
     if (lmax > 0) {
         const ld need = 70 * std::log(2.0L) / (-(ld)k::kIirModalChunk * 64 * std::log(lmax));
         J = std::max(1, (int)std::ceil(need));
     }
     if (J > k::kIirModalJmax) return fail("decays too slowly for the look-back");
+    {
+        auto mat_inf = [&](const std::vector<double>& X, int rows, int cols) {
+            ld r = 0;
+            for (int i = 0; i < rows; i++) {
+                ld s = 0;
+                for (int j = 0; j < cols; j++) s += std::fabs((ld)X[(size_t)i * cols + j]);
+                r = std::max(r, s);
+            }
+            return r;
+        };
+        const ld cond = std::max((ld)1, mat_inf(f.to_v, 2 * M, D) * mat_inf(f.from_v, D, 2 * M));
+        // per section: P = A^2048 (squarings), then ||A^(2048 i)|| for i = 1, 2, ..
+        std::vector<std::array<ld, 4>> U(M), Pw(M);
+        for (int m = 0; m < M; m++) {
+            std::array<ld, 4> b = {A11[m], A12[m], 1, 0};
+            for (int s = 0; s < 11; s++)
+                b = {b[0] * b[0] + b[1] * b[2], b[0] * b[1] + b[1] * b[3], b[2] * b[0] + b[3] * b[2],
+                     b[2] * b[1] + b[3] * b[3]};
+            U[m] = b;                                    // A^2048
+            Pw[m] = {1, 0, 0, 1};
+        }
+        // tail[i] = max_m sum_{i' >= i} ||A_m^(2048 i')||, over i up to the point
+        // where the terms are negligible (or kIirModalJmax + 1, where it fails)
+        const int imax = k::kIirModalJmax + 64;
+        std::vector<ld> term((size_t)imax + 1, 0);
+        for (int m = 0; m < M; m++) {
+            std::array<ld, 4> p = {1, 0, 0, 1};
+            for (int i = 0; i <= imax; i++) {
+                const ld nrm = std::max(std::fabs(p[0]) + std::fabs(p[1]), std::fabs(p[2]) + std::fabs(p[3]));
+                term[(size_t)i] = std::max(term[(size_t)i], nrm);
+                const std::array<ld, 4>& b = U[m];
+                p = {p[0] * b[0] + p[1] * b[2], p[0] * b[1] + p[1] * b[3], p[2] * b[0] + p[3] * b[2],
+                     p[2] * b[1] + p[3] * b[3]};
+            }
+        }
+        std::vector<ld> tail((size_t)imax + 2, 0);
+        {   // beyond imax: a geometric continuation at the last ratio (no decay: no bound)
+            const ld a = term[(size_t)imax], r = term[(size_t)imax - 1] > 0 ? a / term[(size_t)imax - 1] : 0;
+            tail[(size_t)imax + 1] = a == 0 ? 0 : (r < 1 ? a * r / (1 - r) : HUGE_VALL);
+        }
+        for (int i = imax; i >= 0; i--) tail[(size_t)i] = tail[(size_t)i + 1] + term[(size_t)i];
+        const ld lim = std::ldexp((ld)1, -70);
+        while (J <= k::kIirModalJmax && !(cond * tail[(size_t)J] < lim)) J++;
+        if (J > k::kIirModalJmax) return fail("decays too slowly for the look-back (section power bound)");
+    }
     f.J = J;
 
     // powers of the section matrices, [m00, m01, m10, m11] per section
