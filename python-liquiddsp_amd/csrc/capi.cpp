@@ -1837,7 +1837,7 @@ int ldsp_iirfilt_resamp_execute(ldsp_iirfilt_t q, ldsp_resamp_t rs, const void* 
         const Exec e = make_exec(q->device, mem, stream, bd);
         const size_t es = q->cplx ? 8 : 4;
         const bool fuse = n > 0 && q->path_for(n) == IirObj::kModal && rs->sub_len >= 2 &&
-                          rs->sub_len - 1 <= (unsigned)(64 * k::kIirModalChunk);
+                          rs->sub_len - 1 <= 1024u;
         if (!fuse) {
             auto ok = [](int rc) {
                 if (rc != LDSP_OK) throw Error(rc, ldsp_last_error());

@@ -467,27 +467,14 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
             float r = 0.0f;
             if (NC == 2 && f.ctaps) {       // rs_mac: r.x += h.x v.x - h.y v.y, r.y += h.x v.y + h.y v.x
                 const float2* __restrict__ hb = reinterpret_cast<const float2*>(f.sub) + b * f.sub_len;
-                for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
-                    float2 h[8];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : make_float2(0.0f, 0.0f);
-#pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        if (i0 + q < f.sub_len) {
-                            const float vr = at(0, e0 + i0 + q), vi = at(NC - 1, e0 + i0 + q);
-                            r = r + (c == 0 ? h[q].x * vr - h[q].y * vi : h[q].x * vi + h[q].y * vr);
-                        }
+                for (int i = 0; i < f.sub_len; i++) {
+                    const float2 h = hb[i];
+                    const float vr = at(0, e0 + i), vi = at(NC - 1, e0 + i);
+                    r = r + (c == 0 ? h.x * vr - h.y * vi : h.x * vi + h.y * vr);
                 }
             } else {                        // real taps: componentwise (rs_mac_cr / rrrf)
                 const float* __restrict__ hb = f.sub + b * f.sub_len;
-                for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
-                    float h[8];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : 0.0f;
-#pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        if (i0 + q < f.sub_len) r = r + h[q] * at(c, e0 + i0 + q);
-                }
+                for (int i = 0; i < f.sub_len; i++) r = r + hb[i] * at(c, e0 + i);
             }
             f.y[k * NC + c] = r;
         }
@@ -499,53 +486,20 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
     else tile_store<NC, false>(ry, tid, pl);
 }
 
-// One resampler output from a window in LDS (w0[i], w1[i]: component 0 / last of
-// sample i of the window), the resampler kernels' operations in their order; the
-// taps are read 8 at a time ahead of their use (one L2 round trip per 8 taps).
-template <int NC>
-__device__ __forceinline__ void rs_dot(const IirResampFuse& f, size_t b, const float* w0, const float* w1, int c,
-                                       float& r)
-{
-    if (NC == 2 && f.ctaps) {       // rs_mac: r.x += h.x v.x - h.y v.y, r.y += h.x v.y + h.y v.x
-        const float2* __restrict__ hb = reinterpret_cast<const float2*>(f.sub) + b * f.sub_len;
-        for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
-            float2 h[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : make_float2(0.0f, 0.0f);
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-                if (i0 + q < f.sub_len) {
-                    const float vr = w0[i0 + q], vi = w1[i0 + q];
-                    r = r + (c == 0 ? h[q].x * vr - h[q].y * vi : h[q].x * vi + h[q].y * vr);
-                }
-        }
-    } else {                        // real taps: componentwise (rs_mac_cr / rrrf)
-        const float* __restrict__ hb = f.sub + b * f.sub_len;
-        const float* wc = c == 0 ? w0 : w1;
-        for (int i0 = 0; i0 < f.sub_len; i0 += 8) {
-            float h[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) h[q] = i0 + q < f.sub_len ? hb[i0 + q] : 0.0f;
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-                if (i0 + q < f.sub_len) r = r + h[q] * wc[i0 + q];
-        }
-    }
-}
-
 // IIR -> resampler fusion, the outputs whose window straddles a unit boundary:
-// one workgroup per unit u stages the samples [wb - H, wb + H) (unit u - 1's tail,
-// or the resampler history before the call's first sample, and u's head) from
-// the side buffer into LDS and computes the outputs whose window ends in u's
-// first H samples; block 0 also writes the resampler's new history (the call's
-// last H filter outputs).  Same arithmetic and order as the resampler kernels.
+// one thread per unit u, for the outputs whose window ends in u's first H samples
+// (their earlier samples: unit u - 1's tail, or the resampler history before the
+// call's first sample), from the side buffer.  The first such output's window
+// samples and branch taps (up to 64 each) are all loaded before its dot product,
+// so a thread waits for one memory round trip, and the grid is only one thread per
+// 2 048 input samples; any further outputs (rates above ~1.6) take the plain loop.
+// Thread 0 also writes the resampler's new history (the call's last H filter
+// outputs).  Same arithmetic and order as the resampler kernels.
 template <int NC>
-__global__ void __launch_bounds__(64) k_iir_resamp_edges(IirResampFuse f, long n, long nw,
-                                                         const float* __restrict__ hist, float* __restrict__ hist_out)
+__global__ void __launch_bounds__(256) k_iir_resamp_edges(IirResampFuse f, long n, long nw,
+                                                          const float* __restrict__ hist, float* __restrict__ hist_out)
 {
-    extern __shared__ float win[];                  // [NC][2H]
     const int H = f.sub_len - 1;
-    const int lane = threadIdx.x;
     auto sample = [&](long g, int c) -> float {
         if (g < 0) return hist[(g + H) * NC + c];
         const long u = g / kUnit, o = g - u * kUnit;
@@ -554,26 +508,71 @@ __global__ void __launch_bounds__(64) k_iir_resamp_edges(IirResampFuse f, long n
         if (o < min((long)H, cu)) return sd[o * NC + c];
         return sd[(H + o - cu + H) * NC + c];
     };
-    const long u = blockIdx.x;
+    const long u = (long)blockIdx.x * 256 + threadIdx.x;
     if (u == 0)
-        for (int t = lane; t < H; t += 64)
+        for (int t = 0; t < H; t++)
             for (int c = 0; c < NC; c++) hist_out[t * NC + c] = sample(n - H + t, c);
+    if (u >= nw) return;
     const long wb = u * kUnit, cu = min((long)kUnit, n - wb);
-    const int span = H + (int)min((long)H, cu);
-    for (int t = lane; t < span; t += 64)
-        for (int c = 0; c < NC; c++) win[c * 2 * H + t] = sample(wb - H + t, c);
-    __syncthreads();
     const uint64_t kA = resamp_kmin(f.P0, wb, f.step);
     const uint64_t kB = min((uint64_t)f.K, resamp_kmin(f.P0, wb + min((long)H, cu), f.step));
-    for (uint64_t k = kA + lane; k < kB; k += 64) {
+    const bool ct = NC == 2 && f.ctaps;
+    constexpr int kPre = 64;
+    uint64_t k = kA;
+    if (k < kB && f.sub_len <= kPre) {
         const long j = resamp_j(f.P0, k, f.step);
-        const uint64_t ph = f.P0 + k * (uint64_t)f.step - ((uint64_t)j << 24);
-        const size_t b = (size_t)(ph >> f.bits_index);
-        const int o = (int)(j - wb);                // the window's first sample, wb - H + o, sits at win[o]
-        for (int c = 0; c < NC; c++) {
-            float r = 0.0f;
-            rs_dot<NC>(f, b, win + o, win + (NC - 1) * 2 * H + o, c, r);
-            f.y[k * NC + c] = r;
+        const size_t b = (size_t)((f.P0 + k * (uint64_t)f.step - ((uint64_t)j << 24)) >> f.bits_index);
+        float hx[kPre], hy[kPre], v0[kPre], v1[kPre];
+#pragma unroll
+        for (int i = 0; i < kPre; i++) {
+            const int ii = min(i, f.sub_len - 1);
+            if (ct) {
+                const float2 h = reinterpret_cast<const float2*>(f.sub)[b * f.sub_len + ii];
+                hx[i] = h.x;
+                hy[i] = h.y;
+            } else {
+                hx[i] = f.sub[b * f.sub_len + ii];
+            }
+            v0[i] = sample(j - H + ii, 0);
+            v1[i] = sample(j - H + ii, NC - 1);
+        }
+        if (ct) {                   // rs_mac
+            float rx = 0.0f, ry = 0.0f;
+#pragma unroll
+            for (int i = 0; i < kPre; i++)
+                if (i < f.sub_len) {
+                    rx = rx + (hx[i] * v0[i] - hy[i] * v1[i]);
+                    ry = ry + (hx[i] * v1[i] + hy[i] * v0[i]);
+                }
+            f.y[k * NC] = rx;
+            f.y[k * NC + NC - 1] = ry;
+        } else {
+            for (int c = 0; c < NC; c++) {
+                float r = 0.0f;
+#pragma unroll
+                for (int i = 0; i < kPre; i++)
+                    if (i < f.sub_len) r = r + hx[i] * (c == 0 ? v0[i] : v1[i]);
+                f.y[k * NC + c] = r;
+            }
+        }
+        k++;
+    }
+    for (; k < kB; k++) {
+        const long j = resamp_j(f.P0, k, f.step);
+        const size_t b = (size_t)((f.P0 + k * (uint64_t)f.step - ((uint64_t)j << 24)) >> f.bits_index);
+        if (ct) {
+            const float2* __restrict__ hb = reinterpret_cast<const float2*>(f.sub) + b * f.sub_len;
+            float2 r = make_float2(0.0f, 0.0f);
+            for (int i = 0; i < f.sub_len; i++) rs_mac(r, hb[i], make_float2(sample(j - H + i, 0), sample(j - H + i, NC - 1)));
+            f.y[k * NC] = r.x;
+            f.y[k * NC + NC - 1] = r.y;
+        } else {
+            const float* __restrict__ hb = f.sub + b * f.sub_len;
+            for (int c = 0; c < NC; c++) {
+                float r = 0.0f;
+                for (int i = 0; i < f.sub_len; i++) r = r + hb[i] * sample(j - H + i, c);
+                f.y[k * NC + c] = r;
+            }
         }
     }
 }
@@ -604,7 +603,7 @@ void iir_modal_resamp(bool cplx, const IirModalCoef& cf, const void* x, size_t n
     if (n == 0) return;
     LDSP_REQUIRE(cf.M >= 1 && cf.M <= kIirModalMax, "iir: modal form with 1..8 modes");
     LDSP_REQUIRE(p.J >= 1 && p.J <= kIirModalJmax, "iir: look-back depth out of range");
-    LDSP_REQUIRE(f.sub_len >= 2 && f.sub_len - 1 <= kUnit, "iir_resamp: resampler window of 2 .. 2049 samples");
+    LDSP_REQUIRE(f.sub_len >= 2 && f.sub_len - 1 <= 1024, "iir_resamp: resampler window of 2 .. 1025 samples");
 #define LDSP_MODAL(MM)                                                                                        \
     case MM:                                                                                                  \
         if (cplx) launch_modal<2, MM, false, true>(cf, x, n, st_in, st_out, p, nullptr, s, f);                \
@@ -618,13 +617,13 @@ void iir_modal_resamp(bool cplx, const IirModalCoef& cf, const void* x, size_t n
     LDSP_HIP(hipGetLastError());
     const long nw = iir_modal_units(n);
     LDSP_PROF(s, "k_iir_resamp_edges");
-    const size_t lds = (size_t)(cplx ? 2 : 1) * 2 * (f.sub_len - 1) * sizeof(float);
+    const unsigned g = (unsigned)((nw + 255) / 256);
     if (cplx)
-        hipLaunchKernelGGL(k_iir_resamp_edges<2>, dim3((unsigned)nw), dim3(64), lds, s, f, (long)n, nw,
-                           (const float*)hist, (float*)hist_out);
+        hipLaunchKernelGGL(k_iir_resamp_edges<2>, dim3(g), dim3(256), 0, s, f, (long)n, nw, (const float*)hist,
+                           (float*)hist_out);
     else
-        hipLaunchKernelGGL(k_iir_resamp_edges<1>, dim3((unsigned)nw), dim3(64), lds, s, f, (long)n, nw,
-                           (const float*)hist, (float*)hist_out);
+        hipLaunchKernelGGL(k_iir_resamp_edges<1>, dim3(g), dim3(256), 0, s, f, (long)n, nw, (const float*)hist,
+                           (float*)hist_out);
     LDSP_HIP(hipGetLastError());
 }
 

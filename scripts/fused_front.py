@@ -1,6 +1,9 @@
 """IIR -> resampler fusion (liquiddsp.filter_resample) at the bench size: per-kernel
-HIP-event times of the fused front against the two calls on 64 Mi samples, and
-the multi-channel component (8 AMRadio chains on one GPU) with and without it."""
+HIP-event times of the fused front against the two calls on 64 Mi samples
+(`front`), or the multi-channel component (8 AMRadio chains on one GPU) with or
+without it (`channels fused|unfused`; one per process: a second run's streams
+would share hardware queues with the first's).
+    python fused_front.py front | channels fused | channels unfused"""
 import json
 import os
 import sys
@@ -13,6 +16,10 @@ import liquiddsp as L  # noqa: E402
 
 dev = torch.device("cuda", 0)
 n = 64 << 20
+mode = sys.argv[1] if len(sys.argv) > 1 else "front"
+if mode == "channels":
+    print(json.dumps(bench.multi_channel(L, dev, fused=(sys.argv[2] == "fused"))), flush=True)
+    sys.exit(0)
 x = bench.synth_channel(n, 0, dev)
 
 
@@ -34,6 +41,3 @@ out = {"two_calls": timed(lambda: r1.resample(r1.bandpass(x))),
 for k in ("two_calls", "fused"):
     out[k + "_ms"] = round(sum(out[k].values()), 4)
 print(json.dumps(out), flush=True)
-del x
-for fused in (True, False):
-    print(json.dumps(bench.multi_channel(L, dev, fused=fused)), flush=True)

@@ -24,7 +24,7 @@ PKG = os.path.join(REPO, "python-liquiddsp_amd")
 LIBPATH = os.path.join(PKG, "libldsp.so")
 HEADER = os.path.join(REPO, "include", "ldsp.h")
 
-LDSP_EINVAL, LDSP_EHIP = -1, -3
+LDSP_EINVAL, LDSP_EHIP, LDSP_ERANGE = -1, -3, -4
 MEM_HOST = 0
 
 
@@ -313,3 +313,30 @@ def test_ampmodem_type_setter_accepts_ssb(ld):
     assert am.type == "lsb"
     am.carrier = True
     assert (am.type, am.carrier) == ("lsb", True)
+
+
+def test_iirfilt_resamp_checks_before_any_device_work(lib):
+    """ldsp_iirfilt_resamp_execute (liquiddsp.filter_resample's C entry): a real
+    filter with a complex resampler is LDSP_EINVAL, too small an output capacity
+    LDSP_ERANGE with *nout set -- both decided on the host, before any device
+    call (this container has no GPU)."""
+    f, r = C.c_void_p(), C.c_void_p()
+    assert lib.ldsp_iirfilt_create_prototype(2, 0, 8, C.c_float(0.0075), C.c_float(0.0), C.c_float(0.5),
+                                             C.c_float(60.0), 0, C.byref(f)) == 0, lib.ldsp_last_error()
+    assert lib.ldsp_resamp_create(C.c_float(0.024), 20, C.c_float(0.024), C.c_float(60.0), 13, 1, C.byref(r)) == 0
+    x = np.zeros(1000, np.complex64)
+    y = np.zeros(100, np.complex64)
+    nout = C.c_size_t(0)
+    rc = lib.ldsp_iirfilt_resamp_execute(f, r, ptr(x), C.c_size_t(x.size), ptr(y), C.c_size_t(y.size),
+                                         C.byref(nout), 0, None)
+    assert rc == LDSP_EINVAL and b"both be complex" in lib.ldsp_last_error()
+    lib.ldsp_iirfilt_destroy(f)
+    assert lib.ldsp_iirfilt_create_prototype(2, 0, 8, C.c_float(0.0075), C.c_float(0.0), C.c_float(0.5),
+                                             C.c_float(60.0), 1, C.byref(f)) == 0
+    expect = C.c_size_t(0)
+    lib.ldsp_resamp_num_outputs(r, C.c_size_t(100_000), C.byref(expect))
+    rc = lib.ldsp_iirfilt_resamp_execute(f, r, ptr(x), C.c_size_t(100_000), ptr(y), C.c_size_t(10),
+                                         C.byref(nout), 0, None)
+    assert rc == LDSP_ERANGE and nout.value == expect.value > 10
+    lib.ldsp_iirfilt_destroy(f)
+    lib.ldsp_resamp_destroy(r)
