@@ -493,7 +493,7 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
 // samples and branch taps (up to 64 each) are all loaded before its dot product,
 // so a thread waits for one memory round trip, and the grid is only one thread per
 // 2 048 input samples; any further outputs (rates above ~1.6) take the plain loop.
-// Thread 0 also writes the resampler's new history (the call's last H filter
+// Block 0 also writes the resampler's new history (the call's last H filter
 // outputs).  Same arithmetic and order as the resampler kernels.
 template <int NC>
 __global__ void __launch_bounds__(256) k_iir_resamp_edges(IirResampFuse f, long n, long nw,
@@ -509,8 +509,8 @@ __global__ void __launch_bounds__(256) k_iir_resamp_edges(IirResampFuse f, long 
         return sd[(H + o - cu + H) * NC + c];
     };
     const long u = (long)blockIdx.x * 256 + threadIdx.x;
-    if (u == 0)
-        for (int t = 0; t < H; t++)
+    if (blockIdx.x == 0)                            // block 0's threads: the new history, one sample each
+        for (int t = threadIdx.x; t < H; t += 256)
             for (int c = 0; c < NC; c++) hist_out[t * NC + c] = sample(n - H + t, c);
     if (u >= nw) return;
     const long wb = u * kUnit, cu = min((long)kUnit, n - wb);
