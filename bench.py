@@ -548,8 +548,12 @@ def components(L, device, reps=5):
                                      "roof_ms": round(16 * n / HBM_PEAK_GBS / 1e6, 4)}
     del xs
     out["host_buffers"] = host_path(L, device)
-    out["channels_per_gpu"] = multi_channel(L, device, fused=True)
-    out["channels_per_gpu_unfused"] = multi_channel(L, device)
+    # both configurations on the same 16 streams: torch hands out streams from a
+    # pool of 32 per device, so a second set of 16 (after the chain's 4) would wrap
+    # onto streams the first set used and put two channels on one stream
+    strm = [[torch.cuda.Stream(device) for _ in range(2)] for _ in range(8)]
+    out["channels_per_gpu"] = multi_channel(L, device, fused=True, strm=strm)
+    out["channels_per_gpu_unfused"] = multi_channel(L, device, strm=strm)
     return out
 
 
@@ -578,14 +582,15 @@ def exact_chain(L, device, n):
             "iir_kernel": "k_iir_pipe", "note": "exact (bit-identical) mode: the IIR is one sequential recursion"}
 
 
-def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False, fused=False):
+def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False, fused=False, strm=None):
     """SURVEY 8(e)'s caveat: independent channels also share one GPU -- each
     channel's serial PLL walk / AGC repair occupy one CU, so C channels on C
     stream pairs overlap.  Aggregate IQ Msamples/s of `channels` AMRadio chains
     (BASELINE config 4 each, carriers as the ranks of config 5) on this GPU."""
     xs = [synth_channel(n, r, device) for r in range(channels)]
     radios = [AMRadio(L, fused_front=fused) for _ in range(channels)]
-    strm = [[torch.cuda.Stream(device) for _ in range(per)] for _ in range(channels)]
+    if strm is None:
+        strm = [[torch.cuda.Stream(device) for _ in range(per)] for _ in range(channels)]
     # split: the front stages (IIR, resampler, AGC) and the back stages (AmpModem,
     # de-emphasis) of a step on different streams, so that stream order never
     # holds a step's front behind an earlier step's walk
