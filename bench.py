@@ -255,6 +255,9 @@ def main():
     ap.add_argument("--no-kprof", action="store_true",
                     help="no per-kernel HIP events inside the timed steps (kernel times then come from a separate "
                          "profiled pass)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise torch.distributed (RCCL) even at world size 1: the multi-GPU code path "
+                         "(nccl init, barriers, max-over-ranks all-reduce) on a one-GPU box under torch.distributed.run")
     ap.add_argument("--scatter", action="store_true",
                     help="rank 0 holds all channels: every step scatters the IQ blocks and gathers the PCM "
                          "(SURVEY 8e) instead of each rank reading a resident channel")
@@ -263,7 +266,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    dist = world > 1 or (args.dist and "RANK" in os.environ)
     if dist:
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

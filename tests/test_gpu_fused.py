@@ -210,3 +210,27 @@ def test_filter_resample_64Mi_and_host(ld, rng):
     yh = ld.filter_resample(fa, ra, xh)
     assert isinstance(yh, np.ndarray)
     assert np.array_equal(bits(yh), bits(rb(fb(xh))))
+
+
+@pytest.mark.parametrize("rate,fc", [(0.5, 0.2), (1.7, 0.3)])
+def test_filter_resample_other_rates(ld, rng, rate, fc):
+    """Rates where a unit boundary is straddled by many resampler windows (the
+    edge kernel's loop after its prefetched first output) and where a unit holds
+    more than 64 outputs (the fused kernel's output loop): the same bits as the
+    two calls, complex (cccf taps) and real, and the streams continue alike."""
+    import torch
+    n = 300_007
+    for cplx in (True, False):
+        x = cgauss(rng, n) if cplx else rng.standard_normal(n).astype(np.float32)
+        xd = torch.from_numpy(x).cuda()
+        mk = (lambda: (ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2e6),
+                       ld.ComplexResampler(rate=rate, Fc=fc))) if cplx else \
+             (lambda: (ld.RealIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2e6),
+                       ld.RealResampler(rate=rate, Fc=fc)))
+        fa, ra = mk()
+        fb, rb = mk()
+        for a, b in ((0, 5000), (5000, 200_001), (200_001, n)):
+            y = ld.filter_resample(fa, ra, xd[a:b])
+            ref = rb(fb(xd[a:b]))
+            assert y.shape == ref.shape
+            assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), (cplx, a, b)
