@@ -1026,263 +1026,9 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     prev.first = false;
 }
 
-// ---- The whole walker block (8 lane-blocks of 64 entries) as one asm statement.
-// Entries go straight from the LDS ring into v100-v163 (lane-block q: E0 in
-// v[100+8q : 103+8q], E1 in v[104+8q : 107+8q]); each lane-block is the
-// repair loop of walk_lb24 (the next lane-block's offsets carried through it)
-// followed by the store of its repaired outputs with exec = PM -- before the
-// interval test is known.  The test itself is folded lane-wise into acc
-// (saturating x_post - L' - span over the repaired lanes), so no scalar
-// instruction waits on it; one ballot at the end says whether any repaired
-// lane of the block failed.  Then the caller restores the candidates' outputs
-// (record R1.w) at every entry of the block and redoes it lane-block by
-// lane-block from its entry state (walk_lb24, with walk_fallback where needed).
-#define WB_REP(E1X, E1Y, SX, W, SXN, X, XN)                                                                  \
-    "s_ff1_i32_b64 %[j], %[mask]\n\t"                                                                      \
-    "v_readlane_b32 %[dk1], " E1X ", %[j]\n\t"                                                             \
-    "v_readlane_b32 %[dk2], " E1Y ", %[j]\n\t"                                                             \
-    "s_lshl_b64 %[bit], 1, %[j]\n\t"                                                                       \
-    "s_lshl_b64 %[above], -2, %[j]\n\t"                                                                    \
-    "s_or_b64 %[pm], %[pm], %[bit]\n\t"                                                                    \
-    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
-    "v_mad_i32_i24 " X ", " SX ", %[dk1], " X "\n\t"                                                       \
-    "v_add_u32 " X ", %[dk2], " X "\n\t"                                                                   \
-    "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
-    "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
-    "v_cmp_gt_u32_e64 %[mask], " X ", " W "\n\t"                                                           \
-    "v_mad_i32_i24 " XN ", " SXN ", %[dk1], " XN "\n\t"                                                    \
-    "v_add_u32 " XN ", %[dk2], " XN "\n\t"                                                                 \
-    "s_and_b64 %[mask], %[mask], %[above]\n\t"
-// lane-block Q: KC = lgkmcnt that has its own entries and the next one's E0 landed
-// (tuning-build timing variants, k_pll_walk VAR: bit 0 compares against ~0, so no
-// lane-block ever repairs (wrong output); bit 1 drops the per-lane-block store,
-// bit 2 the interval test; the product is VAR 0)
-#define WB_STORE(E1Z)                                                                                      \
-    "s_mov_b64 exec, %[pm]\n\t"                                                                            \
-    "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
-    "s_mov_b64 exec, -1\n\t"
-#define WB_TEST(E0W, E1W)                                                                                  \
-    "v_sub_u32 %[t], %[xp], " E0W "\n\t"                                                                   \
-    "v_cndmask_b32_e64 %[t], 0, %[t], %[pm]\n\t"                                                           \
-    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
-    "v_or_b32 %[acc], %[acc], %[t]\n\t"
-#define WB_LB_(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN, CMPW, STORE, TEST)           \
-    "s_waitcnt lgkmcnt(" KC ")\n\t"                                                                        \
-    "v_mul_lo_u32 %[t], %[d], " N0Z "\n\t"                                                                 \
-    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
-    "v_lshlrev_b32 %[off], 2, " E0Z "\n\t"                                                                 \
-    "s_mov_b64 %[pm], 0\n\t"                                                                               \
-    "s_cmp_eq_u64 %[mask], 0\n\t"                                                                          \
-    "s_cbranch_scc1 2f\n"                                                                                  \
-    "1:\n\t"                                                                                               \
-    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
-    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
-    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc0 2f\n\t"                                         \
-    WB_REP(E1X, E1Y, E0Z, E0Y, N0Z, X, XN) "s_cbranch_scc1 1b\n"                                           \
-    "2:\n\t"                                                                                               \
-    "v_cmp_gt_u32_e64 %[mask], " XN ", " CMPW "\n\t"                                                       \
-    STORE TEST                                                                                             \
-    "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
-    "s_add_u32 %[nrep], %[nrep], %[nr]\n\t"
-#define WB_LB(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN)                           \
-    WB_LB_(Q, KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN, N0Y, WB_STORE(E1Z), WB_TEST(E0W, E1W))
-#define WB_LBQ(Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN)                                            \
-    WB_LB(Q, KC, "v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN)
-#ifdef LDSP_TUNING
-#define WB_LBV(Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, CMPW, STORE, TEST)                          \
-    WB_LB_(Q, KC, "v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, \
-           CMPW, STORE, TEST)
-#endif
-
-#define WB_READS                                                                                           \
-    "ds_read_b128 v[100:103], %[la]\n\t"                                                                   \
-    "ds_read_b128 v[104:107], %[la] offset:8192\n\t"                                                       \
-    "ds_read_b128 v[108:111], %[la] offset:1024\n\t"                                                       \
-    "ds_read_b128 v[112:115], %[la] offset:9216\n\t"                                                       \
-    "ds_read_b128 v[116:119], %[la] offset:2048\n\t"                                                       \
-    "ds_read_b128 v[120:123], %[la] offset:10240\n\t"                                                      \
-    "ds_read_b128 v[124:127], %[la] offset:3072\n\t"                                                       \
-    "ds_read_b128 v[128:131], %[la] offset:11264\n\t"                                                      \
-    "ds_read_b128 v[132:135], %[la] offset:4096\n\t"                                                       \
-    "ds_read_b128 v[136:139], %[la] offset:12288\n\t"                                                      \
-    "ds_read_b128 v[140:143], %[la] offset:5120\n\t"                                                       \
-    "ds_read_b128 v[144:147], %[la] offset:13312\n\t"                                                      \
-    "ds_read_b128 v[148:151], %[la] offset:6144\n\t"                                                       \
-    "ds_read_b128 v[152:155], %[la] offset:14336\n\t"                                                      \
-    "ds_read_b128 v[156:159], %[la] offset:7168\n\t"                                                       \
-    "ds_read_b128 v[160:163], %[la] offset:15360\n\t"                                                      \
-    "v_mov_b32 %[acc], 0\n\t"                                                                              \
-    "s_waitcnt lgkmcnt(15)\n\t"                                                                            \
-    "v_mul_lo_u32 %[t], %[d], v102\n\t"                                                                    \
-    "v_add3_u32 %[xa], v100, %[kb], %[t]\n\t"
-#define WB_OUTS                                                                                            \
-    : [xa] "=&v"(xa), [xb] "=&v"(xb), [xp] "=&v"(xp), [t] "=&v"(t), [off] "=&v"(off), [s7] "=&v"(srel7),     \
-      [mask] "=&s"(mask), [pm] "=&s"(pm), [bad] "=&s"(bad), [bit] "=&s"(bit), [above] "=&s"(above),           \
-      [kb] "+s"(Kb), [d] "+s"(D), [nrep] "+s"(nrep), [acc] "=&v"(acc),                                        \
-      [j] "=&s"(j), [dk1] "=&s"(dk1), [dk2] "=&s"(dk2), [nr] "=&s"(nr)
-#define WB_CLOBBERS                                                                                        \
-    : "scc", "exec", "memory", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",  \
-      "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",   \
-      "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135",   \
-      "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148",   \
-      "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161",   \
-      "v162", "v163"
-
-// Returns nonzero when a repaired lane of the block failed its interval test.
-__device__ __forceinline__ bool walk_blk8(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep,
-                                          uint32_t& srel7)
-{
-    uint32_t xa, xb, xp, t, off, acc, j, dk1, dk2, nr;
-    unsigned long long mask, pm, bad, bit, above;
-    asm volatile(
-        WB_READS
-        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n\t"
-        WB_LBQ("0", "13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]")
-        WB_LBQ("1", "11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]")
-        WB_LBQ("2", "9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]")
-        WB_LBQ("3", "7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]")
-        WB_LBQ("4", "5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]")
-        WB_LBQ("5", "3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]")
-        WB_LBQ("6", "1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]")
-        WB_LBQ("7", "0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]")
-        "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"
-        "v_mov_b32 %[s7], v158"
-        WB_OUTS
-        : [la] "v"(lds), [yb] "s"(yb)
-        WB_CLOBBERS);
-    return bad != 0;
-}
-
-#ifdef LDSP_TUNING
-// Timing variants of walk_blk8 (k_pll_walk VAR bits 0-2, see WB_LB_; wrong outputs).
-#define SEL_CMP_0(n1) n1
-#define SEL_CMP_1(n1) "%[ones]"
-#define SEL_ST_0(e1z) WB_STORE(e1z)
-#define SEL_ST_1(e1z) ""
-#define SEL_TE_0(e0w, e1w) WB_TEST(e0w, e1w)
-#define SEL_TE_1(e0w, e1w) ""
-#define WB_LBS(C, S, T, Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN)                                   \
-    WB_LBV(Q, KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, SEL_CMP_##C("v" #n1), SEL_ST_##S("v" #g),      \
-           SEL_TE_##T("v" #d, "v" #h))
-#define DEF_WALK_BLK8(NAME, C, S, T)                                                                       \
-    __device__ __forceinline__ bool NAME(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep, \
-                                         uint32_t& srel7)                                                  \
-    {                                                                                                      \
-        uint32_t xa, xb, xp, t, off, acc, j, dk1, dk2, nr;                                                 \
-        unsigned long long mask, pm, bad, bit, above;                                                      \
-        const uint32_t ones = ~0u;                                                                         \
-        asm volatile(WB_READS "v_cmp_gt_u32_e64 %[mask], %[xa], " SEL_CMP_##C("v101") "\n\t"                 \
-                     WB_LBS(C, S, T, "0", "13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]") \
-                     WB_LBS(C, S, T, "1", "11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]") \
-                     WB_LBS(C, S, T, "2", "9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]") \
-                     WB_LBS(C, S, T, "3", "7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]") \
-                     WB_LBS(C, S, T, "4", "5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]") \
-                     WB_LBS(C, S, T, "5", "3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]") \
-                     WB_LBS(C, S, T, "6", "1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]") \
-                     WB_LBS(C, S, T, "7", "0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]") \
-                     "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"                                               \
-                     "v_mov_b32 %[s7], v158" WB_OUTS                                                       \
-                     : [la] "v"(lds), [yb] "s"(yb), [ones] "v"(ones) WB_CLOBBERS);                         \
-        return bad != 0;                                                                                   \
-    }
-DEF_WALK_BLK8(walk_blk8_v1, 1, 0, 0)
-DEF_WALK_BLK8(walk_blk8_v2, 0, 1, 0)
-DEF_WALK_BLK8(walk_blk8_v3, 1, 1, 0)
-DEF_WALK_BLK8(walk_blk8_v4, 0, 0, 1)
-DEF_WALK_BLK8(walk_blk8_v5, 1, 0, 1)
-DEF_WALK_BLK8(walk_blk8_v6, 0, 1, 1)
-DEF_WALK_BLK8(walk_blk8_v7, 1, 1, 1)
-#endif
-
-// Pipelined lane-block masks: each lane-block computes the NEXT lane-block's event
-// mask (MN) at its start from the carried offsets and again after every repair, so
-// the next lane-block's s_cmp reads a mask written many instructions earlier
-// instead of waiting for a v_cmp -> SALU hand-off at every lane-block boundary.
-#define WB_REP2(E1X, E1Y, SX, W, SXN, WN, X, XN, M, MN)                                                    \
-    "s_ff1_i32_b64 %[j], " M "\n\t"                                                                        \
-    "v_readlane_b32 %[dk1], " E1X ", %[j]\n\t"                                                             \
-    "v_readlane_b32 %[dk2], " E1Y ", %[j]\n\t"                                                             \
-    "s_lshl_b64 %[bit], 1, %[j]\n\t"                                                                       \
-    "s_lshl_b64 %[above], -2, %[j]\n\t"                                                                    \
-    "s_or_b64 %[pm], %[pm], %[bit]\n\t"                                                                    \
-    "v_cndmask_b32_e64 %[xp], %[xp], " X ", %[bit]\n\t"                                                    \
-    "v_mad_i32_i24 " X ", " SX ", %[dk1], " X "\n\t"                                                       \
-    "v_add_u32 " X ", %[dk2], " X "\n\t"                                                                   \
-    "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
-    "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
-    "v_cmp_gt_u32_e64 " M ", " X ", " W "\n\t"                                                             \
-    "v_mad_i32_i24 " XN ", " SXN ", %[dk1], " XN "\n\t"                                                    \
-    "v_add_u32 " XN ", %[dk2], " XN "\n\t"                                                                 \
-    "v_cmp_gt_u32_e64 " MN ", " XN ", " WN "\n\t"                                                          \
-    "s_and_b64 " M ", " M ", %[above]\n\t"
-#define WB_LB2(KC, E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, N0Z, X, XN, M, MN)                       \
-    "s_waitcnt lgkmcnt(" KC ")\n\t"                                                                        \
-    "v_mul_lo_u32 %[t], %[d], " N0Z "\n\t"                                                                 \
-    "v_add3_u32 " XN ", " N0X ", %[kb], %[t]\n\t"                                                          \
-    "v_lshlrev_b32 %[off], 2, " E0Z "\n\t"                                                                 \
-    "s_mov_b64 %[pm], 0\n\t"                                                                               \
-    "v_cmp_gt_u32_e64 " MN ", " XN ", " N0Y "\n\t"                                                         \
-    "s_cmp_eq_u64 " M ", 0\n\t"                                                                            \
-    "s_cbranch_scc1 2f\n"                                                                                  \
-    "1:\n\t"                                                                                               \
-    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc0 2f\n\t"                            \
-    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc0 2f\n\t"                            \
-    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc0 2f\n\t"                            \
-    WB_REP2(E1X, E1Y, E0Z, E0Y, N0Z, N0Y, X, XN, M, MN) "s_cbranch_scc1 1b\n"                              \
-    "2:\n\t"                                                                                               \
-    WB_STORE(E1Z) WB_TEST(E0W, E1W)                                                                        \
-    "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
-    "s_add_u32 %[nrep], %[nrep], %[nr]\n\t"
-#define WB_LB2Q(KC, a, b, c, d, e, f, g, h, n0, n1, n2, X, XN, M, MN)                                       \
-    WB_LB2(KC, "v" #a, "v" #b, "v" #c, "v" #d, "v" #e, "v" #f, "v" #g, "v" #h, "v" #n0, "v" #n1, "v" #n2, X, XN, M, MN)
-
-__device__ __forceinline__ bool walk_blk8_p(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep,
-                                            uint32_t& srel7)
-{
-    uint32_t xa, xb, xp, t, off, acc, j, dk1, dk2, nr;
-    unsigned long long mask, maskb, pm, bad, bit, above;
-    asm volatile(
-        WB_READS
-        "v_cmp_gt_u32_e64 %[mask], %[xa], v101\n\t"
-        WB_LB2Q("13", 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
-        WB_LB2Q("11", 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
-        WB_LB2Q("9", 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 126, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
-        WB_LB2Q("7", 124, 125, 126, 127, 128, 129, 130, 131, 132, 133, 134, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
-        WB_LB2Q("5", 132, 133, 134, 135, 136, 137, 138, 139, 140, 141, 142, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
-        WB_LB2Q("3", 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 150, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
-        WB_LB2Q("1", 148, 149, 150, 151, 152, 153, 154, 155, 156, 157, 158, "%[xa]", "%[xb]", "%[mask]", "%[mb]")
-        WB_LB2Q("0", 156, 157, 158, 159, 160, 161, 162, 163, 156, 157, 158, "%[xb]", "%[xa]", "%[mb]", "%[mask]")
-        "v_cmp_ne_u32_e64 %[bad], 0, %[acc]\n\t"
-        "v_mov_b32 %[s7], v158"
-        WB_OUTS, [mb] "=&s"(maskb)
-        : [la] "v"(lds), [yb] "s"(yb)
-        WB_CLOBBERS);
-    return bad != 0;
-}
-
-template <int VAR>
-__device__ __forceinline__ bool walk_blk8_sel(uint32_t lds, float* yb, uint32_t& Kb, uint32_t& D, uint32_t& nrep,
-                                              uint32_t& srel7)
-{
-    if (VAR & 16) return walk_blk8_p(lds, yb, Kb, D, nrep, srel7);
-#ifdef LDSP_TUNING
-    switch (VAR & 7) {
-    case 1: return walk_blk8_v1(lds, yb, Kb, D, nrep, srel7);
-    case 2: return walk_blk8_v2(lds, yb, Kb, D, nrep, srel7);
-    case 3: return walk_blk8_v3(lds, yb, Kb, D, nrep, srel7);
-    case 4: return walk_blk8_v4(lds, yb, Kb, D, nrep, srel7);
-    case 5: return walk_blk8_v5(lds, yb, Kb, D, nrep, srel7);
-    case 6: return walk_blk8_v6(lds, yb, Kb, D, nrep, srel7);
-    case 7: return walk_blk8_v7(lds, yb, Kb, D, nrep, srel7);
-    default: break;
-    }
-#endif
-    return walk_blk8(lds, yb, Kb, D, nrep, srel7);
-}
-
 // ---- The walker's block loop as one asm statement (product path).  Per walker
 // block c (entries already in v100-v163, LB0's offsets / events carried in from
-// the previous block): the 8 lane-blocks of walk_blk8, each followed by the LDS
+// the previous block): the 8 lane-blocks (WL_LB), each followed by the LDS
 // reads of the NEXT block's entries of that lane-block into its own registers
 // (free once it is done), so no block starts by waiting for the LDS; block
 // c + 1's header (its sample base) is read at the start of block c and its first
@@ -1597,8 +1343,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     uint32_t S = 0;
     PrevLB prev{0u, 1, 0u, true};
     unsigned long long cyc_walk = 0, cyc_wait = 0;
-    unsigned long long clk_walk = 0, clk_wait = 0;          // VAR & 8 (tuning): shader clocks
-    if constexpr (F24 && !STATS && (VAR == 0 || VAR >= 32)) {
+    static_assert(VAR == 0 || VAR == 32 || VAR == 64 || VAR == 96, "walker variant");
+    if constexpr (F24 && !STATS) {
         // the product path: the block loop in one asm statement (walk_asm_loop)
         if (wave != 0) {
             for (long c = 0; c < nblk; c++) {
@@ -1665,9 +1411,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             S = w.S;
         }
     }
-    for (long c = 0; c < ((F24 && !STATS && (VAR == 0 || VAR >= 32)) ? 0 : nblk); c++) {
+    for (long c = 0; c < ((F24 && !STATS) ? 0 : nblk); c++) {
         const unsigned long long t0 = STATS ? wall_clock64() : 0;
-        const unsigned long long c0 = (VAR & 8) ? __builtin_amdgcn_s_memtime() : 0;
         if (wave != 0) {
             // slot (c + kRing - 1) % kRing held block c - 1, released by the previous barrier
             if (c + kRing - 1 < nblk) walk_dma(buf[(c + kRing - 1) % kRing], cb, c + kRing - 1, lw, lane);
@@ -1682,39 +1427,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
             // software-pipelined LDS reads: the next lane-block's entries are always
             // fetched (clamped), so every wait is the same lgkmcnt
             uint4 A0 = b.e[0][lane], A1 = b.e[1][lane];
-            if constexpr (F24 && !STATS) {
-                float* yb = y + S;
-                const uint32_t Kb0 = rfl(g.Kb), D0 = rfl(g.D), nrep0 = rfl(g.nrep);
-                uint32_t Kb = Kb0, D = D0, nrep = nrep0, s7;
-                const bool bad = walk_blk8_sel<VAR>((uint32_t)(uintptr_t)&b.e[0][lane], yb, Kb, D, nrep, s7);
-                g.Kb = Kb;
-                g.D = D;
-                g.nrep = nrep;
-                if (__builtin_expect(bad, 0)) {
-                    // undo the block's speculative stores (candidate outputs at every
-                    // entry), then redo it lane-block by lane-block from its entry state
-                    // (each rewrite of a sample lands after the previous one: vmcnt(0))
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    for (int q = 0; q < kBlkE / 64; q++) {
-                        const uint32_t sr = b.e[0][q * 64 + lane].z;
-                        if (q * 64 + lane < cnt) y[S + sr] = __uint_as_float(cb.rec[(long)S + sr].w);
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    g.Kb = Kb0;
-                    g.D = D0;
-                    g.nrep = nrep0;
-                    for (int q = 0; q < kBlkE / 64; q++) {
-                        const uint4 C0 = b.e[0][q * 64 + lane], C1 = b.e[1][q * 64 + lane];
-                        const uint4 N0 = b.e[0][min(q + 1, kBlkE / 64 - 1) * 64 + lane];
-                        uint32_t x = C0.x + g.Kb + C0.z * g.D;
-                        unsigned long long mk = __builtin_amdgcn_ballot_w64(x > C0.y);
-                        walk_lb24<false>(C0, C1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane, x, mk, N0.x,
-                                         N0.z, N0.y, yb);
-                    }
-                } else {
-                    prev = PrevLB{s7, min(64, cnt - (kBlkE - 64)), S, false};
-                }
-            } else if constexpr (F24) {
+            if constexpr (F24) {
                 // entries two lane-blocks ahead: lane-block q + 1's E0 feeds q's asm.
                 // Straight-line over all 8 lane-blocks: the last block's tail is
                 // padded with W = ~0 (k_pll_entries), where nothing is ever repaired.
@@ -1748,15 +1461,9 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         // LDS-only barrier: __syncthreads() would also drain the loaders' global fetch of
         // block c + 2 (vmcnt(0)), putting an HBM round trip into every block
         const unsigned long long t1 = STATS ? wall_clock64() : 0;
-        const unsigned long long c1 = (VAR & 8) ? __builtin_amdgcn_s_memtime() : 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (VAR & 8) {
-            const unsigned long long c2 = __builtin_amdgcn_s_memtime();
-            clk_walk += c1 - c0;
-            clk_wait += c2 - c1;
-        }
         if (STATS) {
             const unsigned long long t2 = wall_clock64();
             cyc_walk += t1 - t0;
@@ -1772,10 +1479,6 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         cb.stats[0] = g.nrep;
         cb.stats[1] = g.nfb;
         cb.stats[4] = NE;
-        if (VAR & 8) {
-            cb.stats[2] = clk_walk;
-            cb.stats[3] = clk_wait;
-        }
         if (STATS) {
             cb.stats[2] = cyc_walk;
             cb.stats[3] = cyc_wait;
@@ -1980,9 +1683,7 @@ void pll_back(const PllCall& c, hipStream_t s)
             if (!stats && var > 0) {
 #define WALK_VAR(V) case V: hipLaunchKernelGGL((k_pll_walk<true, false, V>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y); break;
                 switch (var) {
-                WALK_VAR(1) WALK_VAR(2) WALK_VAR(3) WALK_VAR(4) WALK_VAR(5) WALK_VAR(6) WALK_VAR(7)
-                WALK_VAR(8) WALK_VAR(9) WALK_VAR(10) WALK_VAR(11) WALK_VAR(12) WALK_VAR(13) WALK_VAR(14) WALK_VAR(15)
-                WALK_VAR(16) WALK_VAR(24) WALK_VAR(32) WALK_VAR(64) WALK_VAR(96)
+                WALK_VAR(32) WALK_VAR(64) WALK_VAR(96)
                 default: break;
                 }
 #undef WALK_VAR

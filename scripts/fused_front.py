@@ -3,7 +3,7 @@ HIP-event times of the fused front against the two calls on 64 Mi samples
 (`front`), or the multi-channel component (8 AMRadio chains on one GPU) with or
 without it (`channels fused|unfused`; one per process: a second run's streams
 would share hardware queues with the first's).
-    python fused_front.py front | channels fused | channels unfused"""
+    python fused_front.py front | channels fused|unfused [streams per channel]"""
 import json
 import os
 import sys
@@ -18,7 +18,8 @@ dev = torch.device("cuda", 0)
 n = 64 << 20
 mode = sys.argv[1] if len(sys.argv) > 1 else "front"
 if mode == "channels":
-    print(json.dumps(bench.multi_channel(L, dev, fused=(sys.argv[2] == "fused"))), flush=True)
+    per = int(sys.argv[3]) if len(sys.argv) > 3 else 2       # streams per channel
+    print(json.dumps(bench.multi_channel(L, dev, fused=(sys.argv[2] == "fused"), per=per)), flush=True)
     sys.exit(0)
 x = bench.synth_channel(n, 0, dev)
 

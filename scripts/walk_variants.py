@@ -2,9 +2,9 @@
 LDSP_PKG_DIR=build_tuning).  The AmpModem input of the bench chain (BASELINE
 C4: 64 Mi IQ -> IIR -> resampler -> AGC, 1.61 M samples) is demodulated by a
 fresh AmpModem per variant, 5 calls, walker time averaged over calls 2-5.
-LDSP_WALK_VARIANT: bit 0 no repairs (compare against ~0), bit 1 no per-lane-block
-store, bit 2 no interval test (bits 0-2 give wrong outputs: timing only); bit 3
-shader-clock counters (walking / barrier wait) -- output unchanged."""
+LDSP_WALK_VARIANT (the block-loop asm, walk_asm_loop<VAR / 32>): 0 product, 32 no
+repairs, 64 no per-lane-block store (32 and 64 give wrong outputs: timing only), 96
+the store issued by a helper wave's scratch slot (timing only)."""
 import json
 import os
 import sys
@@ -23,7 +23,7 @@ r = AMRadio(L)
 a = r.agc(r.resample(r.bandpass(x)))
 torch.cuda.synchronize()
 del x
-variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,8,9,10,12,11,13,14,15,0".split(","))]
+variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,32,64,96,0".split(","))]
 ref = None
 out = {}
 for v in variants:
