@@ -242,7 +242,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=64 * 1024 * 1024)
+    # (--iq-samples under torch.distributed.run, whose parser takes "--n" for a prefix of its own options)
+    ap.add_argument("--n", "--iq-samples", dest="n", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-components", action="store_true")
@@ -585,7 +586,8 @@ def exact_chain(L, device, n):
             "iir_kernel": "k_iir_pipe", "note": "exact (bit-identical) mode: the IIR is one sequential recursion"}
 
 
-def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False, fused=False, strm=None):
+def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False, fused=False, strm=None,
+                  prio=False):
     """SURVEY 8(e)'s caveat: independent channels also share one GPU -- each
     channel's serial PLL walk / AGC repair occupy one CU, so C channels on C
     stream pairs overlap.  Aggregate IQ Msamples/s of `channels` AMRadio chains
@@ -597,7 +599,9 @@ def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=Fals
     # split: the front stages (IIR, resampler, AGC) and the back stages (AmpModem,
     # de-emphasis) of a step on different streams, so that stream order never
     # holds a step's front behind an earlier step's walk
-    back = [[torch.cuda.Stream(device) for _ in range(per)] for _ in range(channels)] if split else None
+    # prio: the back stages' streams at high priority (the serial walk is each channel's long pole)
+    back = [[torch.cuda.Stream(device, priority=-1 if prio else 0) for _ in range(per)] for _ in range(channels)] \
+        if split else None
 
     def step(k, w=None):
         kk = k if k is not None else w
@@ -620,7 +624,7 @@ def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=Fals
     t = timed_steps(step, steps, max(2, per), torch.cuda.synchronize, lambda: None)
     del xs
     return {"channels": channels, "streams_per_channel": per * (2 if split else 1), "split_front_back": split,
-            "fused_front": fused,
+            "fused_front": fused, "back_priority_high": bool(split and prio),
             "steps": steps, "ms_per_step": round(t / steps * 1e3, 3),
             "Msamples_s": round(channels * n * steps / t / 1e6, 1),
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")}

@@ -296,6 +296,13 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
     // up to J predecessors would set the call's latency.
     const long xq = blockIdx.x & 7, xi = blockIdx.x >> 3;
     if (p.one_xcd && xq != 0) return;
+#ifdef LDSP_TUNING
+    // bit 3: stagger the first round of workgroups, in groups of 64 consecutive units of
+    // an XCD's range (so that a unit's predecessors never start later than it), by
+    // (b >> 9) x (variant >> 4) x ~3.4 us
+    if ((p.variant & 8) && blockIdx.x < 2048)
+        for (int i = 0; i < (int)(blockIdx.x >> 9) * (p.variant >> 4); i++) __builtin_amdgcn_s_sleep(127);
+#endif
     long range0 = 0;
     if (!p.one_xcd)
         for (long y = 0; y < xq; y++) range0 += (nw - y + 7) >> 3;

@@ -143,7 +143,8 @@ struct IirModalPlan {
     int one_xcd = 0;      // small call: every unit on the XCD of block 0 (a grid of 8 x units, the
                           // blocks of the other XCDs return at once), so no unit recomputes a predecessor
     int variant = 0;      // tuning builds only (timing experiments, wrong outputs): bit 0 no look-back,
-                          // bit 1 no pass 2, bit 2 no pass 1 / scan
+                          // bit 1 no pass 2, bit 2 no pass 1 / scan; bit 3 stagger the first
+                          // round of workgroups by (variant >> 4) sleeps (outputs unchanged)
 };
 // IIR -> resampler fusion (liquiddsp.filter_resample, k_iir_modal<RS>): each unit's
 // filter outputs stay in LDS and feed the resampler outputs whose sub_len-sample

@@ -3,7 +3,8 @@ HIP-event times of the fused front against the two calls on 64 Mi samples
 (`front`), or the multi-channel component (8 AMRadio chains on one GPU) with or
 without it (`channels fused|unfused`; one per process: a second run's streams
 would share hardware queues with the first's).
-    python fused_front.py front | channels fused|unfused [streams per channel]"""
+    python fused_front.py front | channels fused|unfused [streams per channel] [split] [prio]
+(split: front and back stages on separate streams; prio: the back streams at high priority)"""
 import json
 import os
 import sys
@@ -19,7 +20,8 @@ n = 64 << 20
 mode = sys.argv[1] if len(sys.argv) > 1 else "front"
 if mode == "channels":
     per = int(sys.argv[3]) if len(sys.argv) > 3 else 2       # streams per channel
-    print(json.dumps(bench.multi_channel(L, dev, fused=(sys.argv[2] == "fused"), per=per)), flush=True)
+    print(json.dumps(bench.multi_channel(L, dev, fused=(sys.argv[2] == "fused"), per=per, split="split" in sys.argv[4:],
+                                         prio="prio" in sys.argv[4:])), flush=True)
     sys.exit(0)
 x = bench.synth_channel(n, 0, dev)
 

@@ -28,7 +28,7 @@ def _free_port():
 def test_bench_rccl_world1(scatter):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--dist", "--steps", "3",
-           "--warmup", "1", "--no-cpu-baseline", "--no-components", "--n", str(1 << 22)]
+           "--warmup", "1", "--no-cpu-baseline", "--no-components", "--iq-samples", str(1 << 22)]
     if scatter:
         cmd.append("--scatter")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
