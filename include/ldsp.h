@@ -56,6 +56,18 @@ int ldsp_version(void);
 int ldsp_device_count(int *n);
 int ldsp_stream_synchronize(void *stream);
 
+/* Page-locked host buffers for LDSP_MEM_HOST calls (no reference counterpart:
+ * the reference returns pageable numpy arrays from every __call__,
+ * src/firfilter.hpp:25-35, src/iirfilter.hpp:292-298, src/resampler.hpp:144-152).
+ * An LDSP_MEM_HOST call whose x or y lies in page-locked memory (from here, or
+ * hipHostMalloc / hipHostRegister) copies it by DMA directly instead of through
+ * the library's staging buffer, so a chain of host calls that hands one call's
+ * output to the next skips two host copies per hand-over.  Blocks are pooled:
+ * ldsp_host_free keeps up to 256 MB of them for reuse.  ldsp_host_alloc fails
+ * with LDSP_ENOMEM once 1 GB is handed out (callers then use pageable memory). */
+int ldsp_host_alloc(size_t bytes, void **p);
+int ldsp_host_free(void *p);
+
 /* Test hook: evaluate the loop transcendentals (ldsp_math.hpp) on the device.
  * fn: 0 exp, 1 log, 2 atan2(a, b), 3 tanh, 4 constrain (y as uint32 bits);
  * 5 exp, 6 log through the loops' fast paths (lm_*_loop); 7 atan2(a, b) in its

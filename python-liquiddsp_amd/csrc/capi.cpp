@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -202,6 +204,17 @@ static PinnedPool& pinned_pool(int device)
     return *pools[device];
 }
 
+// Is p page-locked host memory (ldsp_host_alloc, hipHostMalloc, hipHostRegister)?
+// Such buffers are copied by DMA directly (no staging copy on the host).
+static bool host_pinned(const void* p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) == hipSuccess) return a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    return false;
+}
+
 struct Staging {
     static constexpr size_t kPinMax = (size_t)16 << 20;
     DevBuf in, out;                   // per object (device side)
@@ -212,7 +225,10 @@ struct Staging {
     {
         if (!e.host) return x;
         in.ensure(bytes, e.device);
-        if (bytes && bytes <= kPinMax) {
+        if (bytes && host_pinned(x)) {
+            // page-locked input: DMA from it directly (the call ends with a synchronize)
+            LDSP_HIP(hipMemcpyAsync(in.p, x, bytes, hipMemcpyHostToDevice, e.stream));
+        } else if (bytes && bytes <= kPinMax) {
             PinnedPool& pp = pinned_pool(e.device);
             LDSP_HIP(hipEventSynchronize(pp.done()));
             std::memcpy(pp.hin.ensure(bytes), x, bytes);
@@ -231,6 +247,13 @@ struct Staging {
     void finish(const Exec& e, void* y, size_t bytes)
     {
         if (!e.host) return;
+        if (bytes && host_pinned(y)) {
+            LDSP_HIP(hipMemcpyAsync(y, out.p, bytes, hipMemcpyDeviceToHost, e.stream));
+            PinnedPool& pp = pinned_pool(e.device);
+            LDSP_HIP(hipEventRecord(pp.done(), e.stream));
+            LDSP_HIP(hipEventSynchronize(pp.done()));
+            return;
+        }
         if (bytes && bytes <= kPinMax) {
             PinnedPool& pp = pinned_pool(e.device);
             LDSP_HIP(hipMemcpyAsync(pp.hout.ensure(bytes), out.p, bytes, hipMemcpyDeviceToHost, e.stream));
@@ -2749,6 +2772,76 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
         q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, 2 * k * 4);
+    });
+}
+
+// ------------------------------------------------------- page-locked host pool
+// Blocks are whole 64 KB multiples; a request takes the smallest free block that
+// fits and is at most twice its size.  Freed blocks are cached up to kCacheMax
+// (hipHostFree beyond it); at most kLiveMax is handed out at a time.
+namespace {
+struct HostPool {
+    static constexpr size_t kCacheMax = (size_t)256 << 20, kLiveMax = (size_t)1 << 30;
+    std::mutex mu;
+    std::multimap<size_t, void*> free;
+    std::map<void*, size_t> live;
+    size_t cached = 0, out = 0;
+};
+HostPool& host_pool()
+{
+    static HostPool* p = new HostPool();    // never destroyed: frees can come at interpreter teardown
+    return *p;
+}
+} // namespace
+
+int ldsp_host_alloc(size_t bytes, void** p)
+{
+    return guard([&] {
+        LDSP_REQUIRE(p != nullptr, "host_alloc: NULL output pointer");
+        *p = nullptr;
+        const size_t want = (std::max<size_t>(bytes, 1) + 65535) & ~(size_t)65535;
+        HostPool& hp = host_pool();
+        std::lock_guard<std::mutex> lk(hp.mu);
+        if (hp.out + want > HostPool::kLiveMax) throw Error(LDSP_ENOMEM, "host_alloc: page-locked pool exhausted");
+        auto it = hp.free.lower_bound(want);
+        void* b = nullptr;
+        size_t sz = want;
+        if (it != hp.free.end() && it->first <= 2 * want) {
+            b = it->second;
+            sz = it->first;
+            hp.cached -= sz;
+            hp.free.erase(it);
+        } else {
+            if (hipHostMalloc(&b, want, hipHostMallocPortable) != hipSuccess || !b) {
+                (void)hipGetLastError();
+                throw Error(LDSP_ENOMEM, "host_alloc: hipHostMalloc failed");
+            }
+        }
+        hp.live[b] = sz;
+        hp.out += sz;
+        *p = b;
+    });
+}
+
+int ldsp_host_free(void* p)
+{
+    return guard([&] {
+        if (!p) return;
+        HostPool& hp = host_pool();
+        std::lock_guard<std::mutex> lk(hp.mu);
+        auto it = hp.live.find(p);
+        LDSP_REQUIRE(it != hp.live.end(), "host_free: not a block of ldsp_host_alloc");
+        const size_t sz = it->second;
+        hp.live.erase(it);
+        hp.out -= sz;
+        hp.free.emplace(sz, p);
+        hp.cached += sz;
+        while (hp.cached > HostPool::kCacheMax && !hp.free.empty()) {
+            auto big = std::prev(hp.free.end());
+            hp.cached -= big->first;
+            (void)hipHostFree(big->second);
+            hp.free.erase(big);
+        }
     });
 }
 

@@ -101,6 +101,22 @@ py::object dev_empty(size_t n, bool cplx, const py::object& device)
 
 void* tptr(const py::object& t) { return reinterpret_cast<void*>(t.attr("data_ptr")().cast<uintptr_t>()); }
 
+// numpy outputs of host-memory calls: page-locked (ldsp_host_alloc) from 64 KB up, so
+// the call DMAs into them and a following call DMAs out of them without a staging
+// copy (the README chain hands each stage's array to the next); ordinary
+// writeable numpy arrays otherwise alike.  Pageable when the pool is exhausted.
+template <typename T>
+py::array host_array(size_t n)
+{
+    void* p = nullptr;
+    if (n * sizeof(T) >= ((size_t)64 << 10) && ldsp_host_alloc(n * sizeof(T), &p) == LDSP_OK) {
+        py::capsule owner(p, [](void* q) { ldsp_host_free(q); });
+        return py::array_t<T>({(py::ssize_t)n}, {(py::ssize_t)sizeof(T)}, static_cast<T*>(p), owner);
+    }
+    return py::array_t<T>(n);
+}
+py::array host_array(size_t n, bool cplx) { return cplx ? host_array<cf>(n) : host_array<float>(n); }
+
 using carr = py::array_t<cf, py::array::c_style | py::array::forcecast>;
 using farr = py::array_t<float, py::array::c_style | py::array::forcecast>;
 
@@ -118,7 +134,7 @@ py::object run_same(const py::handle& x, bool cin, bool cout, F&& exec)
         carr a = carr::ensure(x);
         if (!a) throw py::error_already_set();
         const size_t n = (size_t)a.size();
-        py::object out = cout ? py::object(py::array_t<cf>(n)) : py::object(py::array_t<float>(n));
+        py::object out = host_array(n, cout);
         void* yp = py::array(out).mutable_data();
         int rc;
         {
@@ -131,7 +147,7 @@ py::object run_same(const py::handle& x, bool cin, bool cout, F&& exec)
     farr a = farr::ensure(x);
     if (!a) throw py::error_already_set();
     const size_t n = (size_t)a.size();
-    py::object out = cout ? py::object(py::array_t<cf>(n)) : py::object(py::array_t<float>(n));
+    py::object out = host_array(n, cout);
     void* yp = py::array(out).mutable_data();
     int rc;
     {
@@ -300,7 +316,7 @@ struct Resampler {
         const size_t n = (size_t)a.size();
         size_t nout = 0;
         check(ldsp_resamp_num_outputs(q, n, &nout));
-        py::array out = cplx ? py::array(py::array_t<cf>(nout)) : py::array(py::array_t<float>(nout));
+        py::array out = host_array(nout, cplx);
         void* yp = out.mutable_data();
         const void* xp = a.data();
         size_t nw = 0;
@@ -375,7 +391,7 @@ struct IIR {
         py::buffer_info bi = py::reinterpret_borrow<py::buffer>(o).request();
         const size_t nbytes = (size_t)bi.size * (size_t)bi.itemsize;
         const size_t n = nbytes / 4;                  // trailing 1-3 bytes dropped, as bytes_to_iq
-        py::array_t<cf> out(n);
+        py::array_t<cf> out = host_array<cf>(n);
         void* yp = out.mutable_data();
         int rc;
         {
@@ -776,7 +792,7 @@ struct FMStereo {
         const size_t n = (size_t)a.size();
         size_t nout = 0;
         check(ldsp_fmstereo_num_outputs(q, n, &nout));
-        py::array_t<float> out(nout);
+        py::array_t<float> out = host_array<float>(nout);
         void* yp = out.mutable_data();
         const void* xp = a.data();
         size_t nw = 0;
@@ -852,7 +868,7 @@ py::object bytes_to_iq(const py::handle& b)
     }
     py::buffer_info bi = py::reinterpret_borrow<py::buffer>(b).request();
     const size_t nbytes = (size_t)bi.size * (size_t)bi.itemsize;
-    py::array_t<cf> out(nbytes / 4);
+    py::array_t<cf> out = host_array<cf>(nbytes / 4);
     void* yp = out.mutable_data();
     int rc;
     {
@@ -1144,7 +1160,7 @@ PYBIND11_MODULE(_liquiddsp, m)
             const size_t n = (size_t)a.size();
             size_t nout = 0;
             check(ldsp_resamp_num_outputs(rs.q, n, &nout));
-            py::array out = c ? py::array(py::array_t<cf>(nout)) : py::array(py::array_t<float>(nout));
+            py::array out = host_array(nout, c);
             void* yp = out.mutable_data();
             const void* xp = a.data();
             size_t nw = 0;
