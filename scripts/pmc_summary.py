@@ -41,9 +41,48 @@ def counters(d, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def shape_key(name, grid):
+    """kernel + template arguments + grid size: one launch shape (the FIR runs
+    launch one kernel at several sizes, whose per-launch averages must not mix)"""
+    m = re.search(r"(k_\w+)(<[^>]*>)?", name)
+    base = (m.group(1) + (m.group(2) or "")) if m else name[:60]
+    return f"{base}@{grid}"
+
+
+def by_shape(root, run):
+    """{shape: {calls, avg_us, fetch_bytes_corrected, write_bytes, hbm_bytes, hbm_GBs}}"""
+    dur = defaultdict(list)
+    for f in glob.glob(os.path.join(root, f"{run}_trace", "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_" not in r["Kernel_Name"]:
+                continue
+            g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+            dur[shape_key(r["Kernel_Name"], g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = {}
+    for counter, field, scale in (("FETCH_SIZE", "fetch_bytes_corrected", 2048.0), ("WRITE_SIZE", "write_bytes", 1024.0)):
+        acc = defaultdict(list)
+        for f in glob.glob(os.path.join(root, f"{run}_{counter.split('_')[0].lower()}", "**", "*counter_collection.csv"),
+                           recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r.get("Counter_Name") == counter and "k_" in r["Kernel_Name"]:
+                    acc[shape_key(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+        for k, v in acc.items():
+            out.setdefault(k, {})[field] = scale * sum(v) / len(v)
+    for k, v in dur.items():
+        out.setdefault(k, {}).update(calls=len(v), avg_us=round(sum(v) / len(v), 2))
+    for e in out.values():
+        if "fetch_bytes_corrected" in e and "write_bytes" in e and "avg_us" in e:
+            e["hbm_bytes"] = e["fetch_bytes_corrected"] + e["write_bytes"]
+            e["hbm_GBs"] = round(e["hbm_bytes"] / (e["avg_us"] * 1e3), 1)
+    return out
+
+
 def main(root):
     res = {}
-    for run in ("bench", "fir"):
+    for run in ("fir", "front"):
+        if glob.glob(os.path.join(root, f"{run}_trace")):
+            res[f"{run}_by_shape"] = by_shape(root, run)
+    for run in ("bench", "fir", "front"):
         st = stats(os.path.join(root, f"{run}_trace"))
         fe = counters(os.path.join(root, f"{run}_fetch"), "FETCH_SIZE")
         wr = counters(os.path.join(root, f"{run}_write"), "WRITE_SIZE")

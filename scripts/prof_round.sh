@@ -23,4 +23,9 @@ run bench_write --pmc WRITE_SIZE --output-format csv -d $out/bench_write -o benc
 run bench_sq --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM --output-format csv -d $out/bench_sq -o bench -- $B
 run fir_fetch --pmc FETCH_SIZE --output-format csv -d $out/fir_fetch -o fir -- $F
 run fir_write --pmc WRITE_SIZE --output-format csv -d $out/fir_write -o fir -- $F
+# the fused front (filter_resample) and its two-call form at 64 Mi (scripts/fused_front.py front)
+R="python3 scripts/fused_front.py front"
+run front_trace --kernel-trace --stats --output-format csv -d $out/front_trace -o front -- $R
+run front_fetch --pmc FETCH_SIZE --output-format csv -d $out/front_fetch -o front -- $R
+run front_write --pmc WRITE_SIZE --output-format csv -d $out/front_write -o front -- $R
 python3 scripts/pmc_summary.py $out > $out/summary.json && cat $out/summary.json
