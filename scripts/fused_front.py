@@ -3,7 +3,7 @@ HIP-event times of the fused front against the two calls on 64 Mi samples
 (`front`), or the multi-channel component (8 AMRadio chains on one GPU) with or
 without it (`channels fused|unfused`; one per process: a second run's streams
 would share hardware queues with the first's).
-    python fused_front.py front | channels fused|unfused [streams per channel] [split] [prio]
+    python fused_front.py front | channels fused|unfused [streams per channel] [split] [prio] [c=<channels>]
 (split: front and back stages on separate streams; prio: the back streams at high priority)"""
 import json
 import os
@@ -20,8 +20,9 @@ n = 64 << 20
 mode = sys.argv[1] if len(sys.argv) > 1 else "front"
 if mode == "channels":
     per = int(sys.argv[3]) if len(sys.argv) > 3 else 2       # streams per channel
-    print(json.dumps(bench.multi_channel(L, dev, fused=(sys.argv[2] == "fused"), per=per, split="split" in sys.argv[4:],
-                                         prio="prio" in sys.argv[4:])), flush=True)
+    ch = [int(a[2:]) for a in sys.argv[4:] if a.startswith("c=")]      # channel count (default 8)
+    print(json.dumps(bench.multi_channel(L, dev, channels=ch[0] if ch else 8, fused=(sys.argv[2] == "fused"), per=per,
+                                         split="split" in sys.argv[4:], prio="prio" in sys.argv[4:])), flush=True)
     sys.exit(0)
 x = bench.synth_channel(n, 0, dev)
 
