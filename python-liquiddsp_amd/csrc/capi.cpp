@@ -2066,7 +2066,12 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
         static const float wmul = LDSP_KNOB_F("LDSP_AGC_WMUL", 20.0f);
         static const float wamul = LDSP_KNOB_F("LDSP_AGC_WAMUL", 40.0f);
-        static const int rounds = LDSP_KNOB("LDSP_AGC_ROUNDS", 3);
+        // repair rounds (flag + run-by-run re-run launches) before the one-wave
+        // verifier, which re-runs whatever a round left: on the bench chain every
+        // repair lands in round 1 (rounds 2-3 found nothing), and with 8 channels
+        // per GPU each launch on a chain waits 0.1-0.2 ms for a slot, so one round
+        // (8 channels 5.62-5.78 vs 5.83-6.24 ms per step, profiles/r04v_channels.txt)
+        static const int rounds = LDSP_KNOB("LDSP_AGC_ROUNDS", 1);
         static const bool nospec = LDSP_KNOB("LDSP_AGC_NOSPEC", 0) != 0;   // A/B: every call from the true state
         const int W = (int)std::min(1 << 18, std::max(256, (int)(wmul / a)));
         const int Wa = (int)std::min(1 << 20, std::max(1024, (int)(wamul / a)));
