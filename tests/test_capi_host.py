@@ -340,3 +340,16 @@ def test_iirfilt_resamp_checks_before_any_device_work(lib):
     assert rc == LDSP_ERANGE and nout.value == expect.value > 10
     lib.ldsp_iirfilt_destroy(f)
     lib.ldsp_resamp_destroy(r)
+
+
+def test_host_pool_without_gpu(lib):
+    """ldsp_host_alloc fails cleanly with no device (LDSP_ENOMEM, NULL; the pybind
+    module then returns pageable arrays), ldsp_host_free(NULL) is a no-op and a
+    pointer the pool never handed out is rejected."""
+    p = C.c_void_p(1)
+    assert lib.ldsp_host_alloc(C.c_size_t(1 << 20), C.byref(p)) == -2
+    assert p.value is None
+    assert lib.ldsp_host_free(None) == 0
+    junk = np.zeros(4, np.float32)
+    assert lib.ldsp_host_free(ptr(junk)) == LDSP_EINVAL
+    assert b"not a block" in lib.ldsp_last_error()
