@@ -33,12 +33,18 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# One dependent repair of the PLL walk (s_ff1 -> exec = lanes above j, 2 readlanes ->
-# 24-bit multiply-add -> add -> compare into VCC -> VCCZ branch), the walker's own
-# loop (unrolled x4) measured alone on MI355X by scripts/ubench/walk_loop.hip (V10:
-# 89.0 shader cycles at 2.39 GHz, profiles/r04h_walk_loop.txt): the serial floor of
-# the walker per repair.  (Round 3's loop, V8: 108.6 cycles = 45.4 ns.)
-REPAIR_FLOOR_NS = 37.3
+# Serial floor of one PLL-walk repair, derived from the hardware's hop latencies and
+# fixed across rounds (it no longer follows the walker's own loop).  A repair is at
+# least the dependent chain  s_ff1 (next event lane j) -> v_readlane (lane j's kicks)
+# -> v_mad (offsets of the later lanes) -> v_add -> v_cmp (their events, into VCC)
+# -> s_ff1.  scripts/ubench/chain_lat.hip measured on MI355X (profiles/r04d_chain_lat.txt):
+# C3  s_ff1 -> v_readlane -> v_add -> v_cmp -> s_and (-> s_ff1)  72 clocks per iteration;
+# the repair has one more VALU -> VALU hop (C5: 56 / 4 = 14 clocks) and no s_and
+# (C0: SALU -> SALU 56 / 4 = 14 clocks), so 72 + 14 - 14 = 72 shader clocks at the
+# 2384 MHz s_memtime clock of the same run = 30.2 ns.  (The walker's loop itself runs
+# a repair in 89 clocks = 37.3 ns, scripts/ubench/walk_loop.hip V10; the walk also
+# pays its lane-block transitions, which this floor does not count.)
+REPAIR_FLOOR_NS = 30.2
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector spec
 
 
@@ -86,19 +92,25 @@ class AMRadio:
         return [("iir", self.bandpass), ("resamp", self.resample), ("agc", self.agc), ("ampmodem", self.am),
                 ("deemph", self.audio_filter)]
 
-    def __call__(self, iq, events=None):
+    def __call__(self, iq, events=None, front_done=None):
+        # front_done: a torch event recorded once the resampler's call is enqueued
+        # (the next step's chain waits for it, bench.py main: pipeline depth)
         x = iq
         if self.fused_front and events is None:
             x = self.L.filter_resample(self.bandpass, self.resample, x)
+            if front_done is not None:
+                front_done.record()
             for st in (self.agc, self.am, self.audio_filter):
                 x = st(x)
             return x
-        for i, (_, st) in enumerate(self.stages()):
+        for i, (name, st) in enumerate(self.stages()):
             if events is not None:
                 events[i][0].record()
             x = st(x)
             if events is not None:
                 events[i][1].record()
+            if name == "resamp" and front_done is not None:
+                front_done.record()
         return x
 
 
@@ -293,17 +305,28 @@ def main():
     barrier = tdist.barrier if dist else (lambda: None)
 
     host = {"t": 0.0, "max": 0.0}
+    # Pipeline depth: each step's chain waits (on the GPU, no host sync) until the
+    # previous step's resampler call is done.  Without it the rotating streams start
+    # every step's IIR at once and the first step's resampler and AGC kernels wait
+    # behind three other full-GPU filter launches (1.1 ms for a
+    # 0.12 ms resampler); with it the filters still run one step ahead of the walks.
+    front = {"ev": None}
 
-    def step(k, w=None, prof=True, rot=nstreams):
+    def step(k, w=None, prof=False, rot=nstreams, walk_only=False):
         # warmup steps rotate over the streams too: the first use of a stream makes torch's
         # caching allocator map fresh 512 MB blocks for it, which must not land in the timed steps
         h0 = time.perf_counter()
-        if k == 0 and prof:
-            L._profile_reset()                 # per-kernel HIP events over exactly the timed steps
+        if k == 0 and (prof or walk_only):
+            L._profile_reset()                 # HIP events over exactly these steps
+            L._profile_only("k_pll_walk" if walk_only else "")
             L._profile_enable(True)
         xin = scatter_channels(x_all, args.n, device) if (args.scatter and dist) else x
         with torch.cuda.stream(streams[(k if k is not None else (w or 0)) % rot]):
-            out["y"] = radio(xin, events[k] if (k is not None and prof) else None)
+            if front["ev"] is not None and rot > 1:
+                torch.cuda.current_stream().wait_event(front["ev"])
+            ev = torch.cuda.Event() if rot > 1 else None
+            out["y"] = radio(xin, events[k] if (k is not None and prof) else None, front_done=ev)
+            front["ev"] = ev
         if args.scatter and dist:
             gather_pcm(out["y"])
         if k is not None:
@@ -319,12 +342,19 @@ def main():
             with torch.cuda.stream(streams[si]):
                 radio(x)
         torch.cuda.synchronize()
-    elapsed = timed_steps(lambda k, w: step(k, w, prof=kp), args.steps, args.warmup, torch.cuda.synchronize, barrier)
+    # The timed steps carry HIP events around the dominant kernel's launches only (the
+    # PLL walk: 2 events per step, on its launch stream, for roofline.ms_per_launch);
+    # per-kernel and per-stage times come from a separate profiled pass over the same
+    # steps right after (events around every launch cost ~0.03 ms per step).
+    elapsed = timed_steps(lambda k, w: step(k, w, walk_only=kp), args.steps, args.warmup, torch.cuda.synchronize,
+                          barrier)
     host_ms = host["t"] / args.steps * 1e3
     host_max_ms = host["max"] * 1e3
-    if not kp:          # kernel / stage times from a separate profiled pass over the same steps
-        timed_steps(step, args.steps, 0, torch.cuda.synchronize, barrier)
     L._profile_enable(False)
+    walk_timed = L._profile_report().get("k_pll_walk")
+    timed_steps(lambda k, w: step(k, w, prof=True), args.steps, 0, torch.cuda.synchronize, barrier)
+    L._profile_enable(False)
+    L._profile_only("")
     kprof = L._profile_report()
     # the same chain with every step on one stream (no overlap between steps), for reference
     single = timed_steps(lambda k, w: step(k, w, prof=False, rot=1), min(args.steps, 5), 1, torch.cuda.synchronize,
@@ -357,6 +387,10 @@ def main():
                          "alg_GBs": round(ab / (per * 1e-3) / 1e9, 2) if ab else None}
     dom = max(kprof, key=lambda k: kprof[k][1])
     dom_ms = kprof[dom][1] / kprof[dom][0]
+    dom_src = "profiled pass after the timed steps"
+    if dom == "k_pll_walk" and walk_timed:
+        dom_ms = walk_timed[1] / walk_timed[0]
+        dom_src = "HIP events around its launches inside the timed steps"
     achieved = alg.get(dom, 0) / (dom_ms * 1e-3) / 1e9
     entries, repairs, fallbacks = radio.am._walk_stats()       # the last call's walk (synchronises)
     res = {
@@ -379,11 +413,12 @@ def main():
                    "carrier_hz": CARRIERS[(rank if args.channel is None else args.channel) % len(CARRIERS)],
                    "seed": 4 if (rank if args.channel is None else args.channel) == 0 else 10 + (rank if args.channel is None else args.channel),
                    "parallelism": f"channel-per-gpu x{world}" + (" rank0-scatter/gather" if args.scatter and dist else "")},
-        "roofline": roofline(dom, dom_ms, achieved, entries, repairs, fallbacks),
+        "roofline": dict(roofline(dom, dom_ms, achieved, entries, repairs, fallbacks), ms_source=dom_src),
         "streams": nstreams,
         "host_ms_per_step": round(host_ms, 4),
         "host_ms_max_step": round(host_max_ms, 4),
-        "kernel_events_in_timed_steps": kp,
+        "kernel_events_in_timed_steps": "k_pll_walk only" if kp else False,
+        "pipeline": "each step waits for the previous step's resampler call (GPU event)" if nstreams > 1 else None,
         "single_stream_ms_per_step": round(single / single_steps * 1e3, 4),
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "kernels": kernels,

@@ -68,6 +68,13 @@ int ldsp_stream_synchronize(void *stream);
 int ldsp_host_alloc(size_t bytes, void **p);
 int ldsp_host_free(void *p);
 
+/* Test hook: the per-thread staging pools of LDSP_MEM_HOST calls.  A thread
+ * takes one pool per device on its first host call and returns it to a
+ * process-wide free list when it exits, so *total (pools ever created) stays at
+ * the number of threads making host calls concurrently; *idle = pools on the
+ * free list. */
+int ldsp_debug_host_pools(size_t *total, size_t *idle);
+
 /* Test hook: evaluate the loop transcendentals (ldsp_math.hpp) on the device.
  * fn: 0 exp, 1 log, 2 atan2(a, b), 3 tanh, 4 constrain (y as uint32 bits);
  * 5 exp, 6 log through the loops' fast paths (lm_*_loop); 7 atan2(a, b) in its
@@ -89,6 +96,8 @@ int ldsp_debug_math_fastcheck(int fn, uint32_t begin, uint32_t end, uint32_t str
  * pair on its stream; the report lists "name calls total_ms" lines. */
 int ldsp_profile_enable(int on);
 int ldsp_profile_reset(void);
+/* time only the launches of the kernel named `kernel` (NULL or "": every kernel) */
+int ldsp_profile_only(const char *kernel);
 int ldsp_profile_report(char *buf, size_t cap, size_t *len);
 
 /* ------------------------------------------------------------------------
@@ -259,6 +268,17 @@ int ldsp_agc_create(ldsp_agc_t *q);
 int ldsp_debug_agc_tsa_perturb(ldsp_agc_t q, int on);
 /* chunks re-run by that in-kernel check since the object was created */
 int ldsp_debug_agc_tsa_reruns(ldsp_agc_t q, unsigned int *count);
+/* Test hooks for chunk-parallel calls (above the small-call range): with
+ * perturb on, every odd chunk starts from its guessed state with the gain 1 ulp
+ * off, so the flag pass marks it and the repair rounds / the verifier re-run it
+ * from its predecessor's true end state (output still bit-identical to
+ * agc_crcf).  rounds: parallel repair rounds before the one-wave verifier (-1 =
+ * the default, 1; 0 = the verifier alone re-runs every flagged chunk).
+ * reruns: chunks re-run since the object was created, by the repair rounds
+ * (*runfix) and by the verifier (*verify). */
+int ldsp_debug_agc_perturb(ldsp_agc_t q, int on);
+int ldsp_debug_agc_rounds(ldsp_agc_t q, int rounds);
+int ldsp_debug_agc_reruns(ldsp_agc_t q, unsigned int *runfix, unsigned int *verify);
 int ldsp_agc_destroy(ldsp_agc_t q);
 int ldsp_agc_reset(ldsp_agc_t q);
 int ldsp_agc_set_bandwidth(ldsp_agc_t q, float bw);

@@ -185,8 +185,12 @@ struct PinnedBuf {
 // object a thread calls on one device (a host-buffer call is synchronous -- it
 // returns only after its output copy -- so a thread's calls never overlap in
 // them).  Grown on demand up to kPinMax each (larger transfers go unpinned), never
-// shrunk, and deliberately not freed at thread exit (hipHostFree at process
-// teardown can outlive the HIP runtime): at most 2 x kPinMax per thread and device.
+// shrunk.  A thread takes a pool from a process-wide free list on its first host
+// call on a device and returns it there when it exits (thread_local holder), so
+// short-lived threads (thread pools, DataLoader workers) reuse pools instead of
+// leaking page-locked memory: the number of pools is bounded by the number of
+// threads making host calls at the same time.  The free list itself is never
+// destroyed (hipHostFree at process teardown can outlive the HIP runtime).
 struct PinnedPool {
     PinnedBuf hin, hout;
     hipEvent_t hin_done = nullptr;    // the last copy out of hin (a call that threw may not have synchronized)
@@ -196,12 +200,47 @@ struct PinnedPool {
         return hin_done;
     }
 };
+namespace {
+struct PoolList {
+    std::mutex mu;
+    std::vector<std::vector<PinnedPool*>> free;    // per device
+    size_t total = 0;                              // pools ever created
+};
+PoolList& pool_list()
+{
+    static PoolList* l = new PoolList();           // never destroyed (see above)
+    return *l;
+}
+struct ThreadPools {
+    std::vector<PinnedPool*> pools;                // this thread's, per device
+    ~ThreadPools()
+    {
+        PoolList& l = pool_list();
+        std::lock_guard<std::mutex> lk(l.mu);
+        for (size_t d = 0; d < pools.size(); d++)
+            if (pools[d]) {
+                if (l.free.size() <= d) l.free.resize(d + 1);
+                l.free[d].push_back(pools[d]);
+            }
+    }
+};
+} // namespace
 static PinnedPool& pinned_pool(int device)
 {
-    thread_local std::vector<PinnedPool*> pools;
-    if ((int)pools.size() <= device) pools.resize(device + 1, nullptr);
-    if (!pools[device]) pools[device] = new PinnedPool();
-    return *pools[device];
+    thread_local ThreadPools tp;
+    if ((int)tp.pools.size() <= device) tp.pools.resize(device + 1, nullptr);
+    if (!tp.pools[device]) {
+        PoolList& l = pool_list();
+        std::lock_guard<std::mutex> lk(l.mu);
+        if ((int)l.free.size() > device && !l.free[device].empty()) {
+            tp.pools[device] = l.free[device].back();
+            l.free[device].pop_back();
+        } else {
+            tp.pools[device] = new PinnedPool();
+            l.total++;
+        }
+    }
+    return *tp.pools[device];
 }
 
 // Is p page-locked host memory (ldsp_host_alloc, hipHostMalloc, hipHostRegister)?
@@ -806,6 +845,8 @@ struct AgcObj {
     StreamMark ord, front, slot[2];
     Staging stg;
     int tsa_perturb = 0;              // ldsp_debug_agc_tsa_perturb (test hook)
+    int perturb = 0;                  // ldsp_debug_agc_perturb (test hook, chunk-parallel calls)
+    int rounds_force = -1;            // ldsp_debug_agc_rounds (test hook; -1: the default)
     void init()
     {
         // agc_crcf_create: bandwidth 0.01, reset (g=1, y2'=1), squelch disabled,
@@ -1045,9 +1086,17 @@ void drain_locked()
 
 bool enabled() { return g_on.load(std::memory_order_relaxed); }
 
+// ldsp_profile_only: time only the launches of one kernel (the bench's timed
+// steps record the dominant kernel alone: two events per launch of it instead
+// of two per launch of every kernel)
+std::atomic<const char*> g_only{nullptr};
+std::string g_only_name;
+
 Scope::Scope(hipStream_t s_, const char* n) : s(s_), name(n)
 {
     if (!enabled()) return;
+    const char* only = g_only.load(std::memory_order_relaxed);
+    if (only && std::strcmp(only, n) != 0) return;
     if (hipEventCreate(&a) != hipSuccess || hipEventRecord(a, s) != hipSuccess) a = nullptr;
 }
 
@@ -1072,6 +1121,16 @@ int ldsp_profile_enable(int on)
 {
     ldsp::prof::g_on.store(on != 0);
     return LDSP_OK;
+}
+
+int ldsp_profile_only(const char* kernel)
+{
+    return guard([&] {
+        std::lock_guard<std::mutex> lk{ldsp::prof::g_mu};
+        ldsp::prof::g_only.store(nullptr);
+        ldsp::prof::g_only_name = kernel ? kernel : "";
+        if (kernel && *kernel) ldsp::prof::g_only.store(ldsp::prof::g_only_name.c_str());
+    });
 }
 
 int ldsp_profile_reset(void)
@@ -1693,6 +1752,30 @@ int ldsp_debug_agc_tsa_perturb(ldsp_agc_t q, int on)
         q->tsa_perturb = on ? 1 : 0;
     });
 }
+int ldsp_debug_agc_perturb(ldsp_agc_t q, int on)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->perturb = on ? 1 : 0;
+    });
+}
+int ldsp_debug_agc_rounds(ldsp_agc_t q, int rounds)
+{
+    return guard([&] {
+        NONNULL(q);
+        LDSP_REQUIRE(rounds >= -1 && rounds <= 6, "agc: rounds must be -1 (default) or 0..6");
+        q->rounds_force = rounds;
+    });
+}
+int ldsp_debug_agc_reruns(ldsp_agc_t q, unsigned int* runfix, unsigned int* verify)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->pull();
+        if (runfix) *runfix = (unsigned)q->h.pad[2];
+        if (verify) *verify = (unsigned)q->h.pad[1];
+    });
+}
 int ldsp_debug_agc_tsa_reruns(ldsp_agc_t q, unsigned int* count)
 {
     return guard([&] {
@@ -1866,9 +1949,22 @@ int ldsp_iirfilt_resamp_execute(ldsp_iirfilt_t q, ldsp_resamp_t rs, const void* 
                 if (rc != LDSP_OK) throw Error(rc, ldsp_last_error());
             };
             if (e.host) {
-                std::vector<char> t(std::max<size_t>(n, 1) * es);
-                ok(ldsp_iirfilt_execute(q, x, n, t.data(), LDSP_MEM_HOST, nullptr));
-                ok(ldsp_resamp_execute(rs, t.data(), n, y, cap, nout, LDSP_MEM_HOST, nullptr));
+                // the hand-over in page-locked memory when the pool has it (the two
+                // calls then DMA it directly), pageable otherwise; the caller's stream
+                const size_t tb = std::max<size_t>(n, 1) * es;
+                void* tp = nullptr;
+                std::vector<char> tv;
+                if (ldsp_host_alloc(tb, &tp) != LDSP_OK) {
+                    tp = nullptr;
+                    tv.resize(tb);
+                }
+                struct Free {
+                    void* p;
+                    ~Free() { if (p) (void)ldsp_host_free(p); }
+                } fr{tp};
+                void* t = tp ? tp : tv.data();
+                ok(ldsp_iirfilt_execute(q, x, n, t, LDSP_MEM_HOST, stream));
+                ok(ldsp_resamp_execute(rs, t, n, y, cap, nout, LDSP_MEM_HOST, stream));
             } else {
                 void* t = q->rsbuf.ensure(std::max<size_t>(n, 1) * es, q->device);
                 ok(ldsp_iirfilt_execute(q, x, n, t, LDSP_MEM_DEVICE, stream));
@@ -2097,7 +2193,8 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         if (n > 0 && (par || tsa)) {
             p.W = tsa ? 0 : W;                 // tsa: every chunk from 1 on is checked against its predecessor
             p.Wa = Wa;
-            p.rounds = tsa ? 1 : std::max(0, std::min(rounds, 6));   // tsa: one run covers the rare deviation
+            p.rounds = tsa ? 1 : std::max(0, std::min(q->rounds_force >= 0 ? q->rounds_force : rounds, 6));
+            // (tsa: one run covers the rare deviation)
             // chunk length: every chunk re-runs Wa + W warm-up steps (6 000 at
             // bandwidth 0.01) for its C outputs, so C = 1024 does a quarter of the
             // front's work of C = 256 at ~20 % more latency (hidden under the PLL
@@ -2120,6 +2217,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             static const bool tsa_sep = LDSP_KNOB("LDSP_AGC_TSA_SEPARATE", 0) != 0;
             p.tsa = tsa ? (p.nchunks <= 64 && !tsa_sep && !LDSP_KNOB("LDSP_DEBUG_AGC", 0) ? 2 : 1) : 0;
             if (p.tsa == 2 && q->tsa_perturb) p.tsa |= 4;
+            if (!tsa && q->perturb) p.tsa |= 8;          // test hook: odd chunks start 1 ulp off
         }
         // the next call's history first: its front then waits for this copy only
         if (n > 0) k::delay_hist(dx, q->hist[h3].p, q->hist[(h3 + 1) % 3].p, n, (int)hl, e.stream);
@@ -2306,6 +2404,11 @@ int ldsp_ampmodem_seq_stats(ldsp_ampmodem_t q, uint64_t* batches, uint64_t* redo
 // Costas: the candidates start from the true state (the loop's two stable
 // points half a turn apart make a guess ambiguous), so its front also waits for
 // call k-1's walk.
+// Calls above kAmpPieceMax samples run as consecutive sub-calls of at most that
+// many (same bits: every stage streams its state across calls): the walker stores
+// repaired outputs through 32-bit byte offsets (k_pll.hip), so one launch covers < 2^30.
+static constexpr size_t kAmpPieceMax = size_t(1) << 29;
+
 static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, float mod_index, int costas, float* mbuf,
                             int out_idx = 0)
 {
@@ -2404,6 +2507,14 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "ampmodem_demodulate: NULL buffer");
+        if (n > kAmpPieceMax) {              // the walker's 32-bit store offsets: consecutive sub-calls
+            for (size_t off = 0; off < n; off += kAmpPieceMax) {
+                const int rc = ldsp_ampmodem_demodulate(q, (const char*)x + off * 8, std::min(kAmpPieceMax, n - off),
+                                                        (char*)y + off * 4, mem, stream);
+                if (rc != LDSP_OK) throw Error(rc, g_last_error);
+            }
+            return;
+        }
         const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
@@ -2490,6 +2601,15 @@ int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void* x, size_t n, void* y, 
     return guard([&] {
         NONNULL(q);
         LDSP_REQUIRE(n == 0 || (x && y), "bcastam_demodulate: NULL buffer");
+        if (n > kAmpPieceMax) {              // as ldsp_ampmodem_demodulate
+            for (size_t off = 0; off < n; off += kAmpPieceMax) {
+                const size_t m = std::min(kAmpPieceMax, n - off);
+                const int rc = ldsp_bcastam_demodulate(q, (const char*)x + off * 8, m, (char*)y + off * 4,
+                                                       pre ? (char*)pre + off * 4 : nullptr, mem, stream);
+                if (rc != LDSP_OK) throw Error(rc, g_last_error);
+            }
+            return;
+        }
         const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
@@ -2806,24 +2926,33 @@ int ldsp_host_alloc(size_t bytes, void** p)
         *p = nullptr;
         const size_t want = (std::max<size_t>(bytes, 1) + 65535) & ~(size_t)65535;
         HostPool& hp = host_pool();
-        std::lock_guard<std::mutex> lk(hp.mu);
-        if (hp.out + want > HostPool::kLiveMax) throw Error(LDSP_ENOMEM, "host_alloc: page-locked pool exhausted");
-        auto it = hp.free.lower_bound(want);
         void* b = nullptr;
         size_t sz = want;
-        if (it != hp.free.end() && it->first <= 2 * want) {
-            b = it->second;
-            sz = it->first;
-            hp.cached -= sz;
-            hp.free.erase(it);
-        } else {
-            if (hipHostMalloc(&b, want, hipHostMallocPortable) != hipSuccess || !b) {
-                (void)hipGetLastError();
-                throw Error(LDSP_ENOMEM, "host_alloc: hipHostMalloc failed");
+        {
+            std::lock_guard<std::mutex> lk(hp.mu);
+            auto it = hp.free.lower_bound(want);
+            // the limit counts the block actually handed out (a cached block may be up to 2x want)
+            if (it != hp.free.end() && it->first <= 2 * want && hp.out + it->first <= HostPool::kLiveMax) {
+                b = it->second;
+                sz = it->first;
+                hp.cached -= sz;
+                hp.free.erase(it);
+                hp.live[b] = sz;
+                hp.out += sz;
+                *p = b;
+                return;
             }
+            if (hp.out + want > HostPool::kLiveMax) throw Error(LDSP_ENOMEM, "host_alloc: page-locked pool exhausted");
+            hp.out += want;                  // reserved while the allocation runs outside the lock
         }
+        if (hipHostMalloc(&b, want, hipHostMallocPortable) != hipSuccess || !b) {
+            (void)hipGetLastError();
+            std::lock_guard<std::mutex> lk(hp.mu);
+            hp.out -= want;
+            throw Error(LDSP_ENOMEM, "host_alloc: hipHostMalloc failed");
+        }
+        std::lock_guard<std::mutex> lk(hp.mu);
         hp.live[b] = sz;
-        hp.out += sz;
         *p = b;
     });
 }
@@ -2833,20 +2962,36 @@ int ldsp_host_free(void* p)
     return guard([&] {
         if (!p) return;
         HostPool& hp = host_pool();
-        std::lock_guard<std::mutex> lk(hp.mu);
-        auto it = hp.live.find(p);
-        LDSP_REQUIRE(it != hp.live.end(), "host_free: not a block of ldsp_host_alloc");
-        const size_t sz = it->second;
-        hp.live.erase(it);
-        hp.out -= sz;
-        hp.free.emplace(sz, p);
-        hp.cached += sz;
-        while (hp.cached > HostPool::kCacheMax && !hp.free.empty()) {
-            auto big = std::prev(hp.free.end());
-            hp.cached -= big->first;
-            (void)hipHostFree(big->second);
-            hp.free.erase(big);
+        std::vector<void*> evict;            // hipHostFree may synchronise the device: never under the lock
+        {
+            std::lock_guard<std::mutex> lk(hp.mu);
+            auto it = hp.live.find(p);
+            LDSP_REQUIRE(it != hp.live.end(), "host_free: not a block of ldsp_host_alloc");
+            const size_t sz = it->second;
+            hp.live.erase(it);
+            hp.out -= sz;
+            hp.free.emplace(sz, p);
+            hp.cached += sz;
+            while (hp.cached > HostPool::kCacheMax && !hp.free.empty()) {
+                auto big = std::prev(hp.free.end());
+                hp.cached -= big->first;
+                evict.push_back(big->second);
+                hp.free.erase(big);
+            }
         }
+        for (void* b : evict) (void)hipHostFree(b);
+    });
+}
+
+int ldsp_debug_host_pools(size_t* total, size_t* idle)
+{
+    return guard([&] {
+        PoolList& l = pool_list();
+        std::lock_guard<std::mutex> lk(l.mu);
+        size_t f = 0;
+        for (const auto& v : l.free) f += v.size();
+        if (total) *total = l.total;
+        if (idle) *idle = f;
     });
 }
 

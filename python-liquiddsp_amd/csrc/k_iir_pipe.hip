@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(kPipeThreads) k_iir_pipe(IirDesc d, const floa
 {
     LDSP_LATENCY_CRITICAL();
     constexpr int R = 3 * kPipeT;                 // output ring (steps), see below
-    __shared__ float xin[2][2][kPipeT + 16];      // [tile parity][component][step - t0] (+ read-ahead padding)
+    __shared__ __attribute__((aligned(16))) float xin[2][2][kPipeT + 16];      // [tile parity][component][step - t0] (+ read-ahead padding)
     __shared__ __attribute__((aligned(16))) float yr[2][R];   // [component][step mod R]: the last lane's output
     __shared__ __attribute__((aligned(16))) float junk[64 * 8];   // the other lanes' output writes
     const int tid = threadIdx.x;

@@ -360,6 +360,69 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
     }
 }
 
+// Approximate loop step for the carrier candidates' warm-up (never for a
+// record or an output).  Its only product is chunk k's start state, a guess the
+// walker corrects through the exact offset whatever it is (a candidate from an
+// exact warm-up is itself only a guess: its offset from the true trajectory
+// settles at ~2^17 and never reaches 0), so the warm-up
+// needs the loop's dynamics, not its bits: the same table cell (the loop's
+// quantisation, which sets where it settles), hardware sin / cos of that cell's
+// angle for the table entries, a minimax atan2 (|error| < 1e-5 rad: a kick
+// error of ~2^8 phase units against the 2^19 margin), and float -> int
+// conversions for constrain (|phi beta| / 2pi < 1/2, so the wrap of a negative
+// kick is the int32 -> uint32 conversion).  ~25 dependent instructions a step
+// instead of ~110 for the exact one (atan2 alone ~70).
+__device__ __forceinline__ float atan2_approx(float y, float x)
+{
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mn * __builtin_amdgcn_rcpf(mx > 0.0f ? mx : 1.0f);
+    const float s = a * a;
+    float r = fmaf(fmaf(fmaf(-0.0464964749f, s, 0.15931422f), s, -0.327622764f), s * a, a);
+    r = ay > ax ? 1.57079637f - r : r;
+    r = x < 0.0f ? 3.14159274f - r : r;
+    return y < 0.0f ? -r : r;
+}
+
+__device__ __forceinline__ void cand_warm_approx(const PllIn& in, long a, long b, float alpha, float beta,
+                                                 uint32_t& theta, uint32_t& d)
+{
+    if (a >= b) return;
+    constexpr float kRadToPhase = 683565275.57643158f;      // 2^32 / (2 pi)
+    const float as = alpha * kRadToPhase, bs = beta * kRadToPhase;
+    const long full = a + (b - a) / kB * kB;
+    float2 nx[kB];
+#pragma unroll
+    for (int j = 0; j < kB; j++) nx[j] = in.x0[min(a + j, b - 1)];
+    long i = a;
+    for (; i < full; i += kB) {
+        float2 cx[kB];
+#pragma unroll
+        for (int j = 0; j < kB; j++) cx[j] = nx[j];
+#pragma unroll
+        for (int j = 0; j < kB; j++) nx[j] = in.x0[min(i + kB + j, b - 1)];
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            const float ang = (float)tidx(theta) * 6.1359231515e-03f;      // 2 pi / 1024
+            const float sn = __sinf(ang), cs = __cosf(ang);
+            // v0 = x0 conj(e^{j ang})
+            const float v0r = fmaf(cx[j].x, cs, cx[j].y * sn), v0i = fmaf(cx[j].y, cs, -(cx[j].x * sn));
+            const float phi = atan2_approx(v0i, v0r);
+            d += (uint32_t)(int)(phi * as);
+            theta += (uint32_t)(int)(phi * bs) + d;
+        }
+    }
+    for (; i < b; i++) {
+        const float2 c = in.x0[i];
+        const float ang = (float)tidx(theta) * 6.1359231515e-03f;
+        const float sn = __sinf(ang), cs = __cosf(ang);
+        const float v0r = fmaf(c.x, cs, c.y * sn), v0i = fmaf(c.y, cs, -(c.x * sn));
+        const float phi = atan2_approx(v0i, v0r);
+        d += (uint32_t)(int)(phi * as);
+        theta += (uint32_t)(int)(phi * bs) + d;
+    }
+}
+
 // Candidate chunk k starts `warm` samples early from the guess state (the
 // previous call's last candidate end state, or the true state after a reset or a
 // sequential call), extrapolated at constant frequency.  The guess is never the
@@ -368,7 +431,7 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
 // from_true: start from the true state instead of the guess (Costas, whose
 // front waits for the previous walk: chunk 0 is then the true trajectory's branch).
 __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st, int gcur, CandBuf cb,
-                                                 float* __restrict__ y, int warm, int from_true)
+                                                 float* __restrict__ y, int warm, int from_true, int approx)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
@@ -388,7 +451,8 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st,
         theta = g_th + (uint32_t)((uint64_t)w0 * d);   // constant-frequency extrapolation
     }
     uint32_t nent = 0;
-    cand_run<false>(in, tab, w0, s0, alpha, beta, theta, d, cb, y, nent);
+    if (approx) cand_warm_approx(in, w0, s0, alpha, beta, theta, d);
+    else cand_run<false>(in, tab, w0, s0, alpha, beta, theta, d, cb, y, nent);
     cb.cs[2 * k] = theta;
     cb.cs[2 * k + 1] = d;
     cand_run<true>(in, tab, s0, s1, alpha, beta, theta, d, cb, y, nent);
@@ -1624,8 +1688,11 @@ void pll_front(const PllCall& c, hipStream_t s)
     {
         LDSP_PROF(s, "k_pll_cand");
         static const int warm = LDSP_KNOB("LDSP_PLL_WARM", kWarm);
+        // carrier loop: approximate warm-up (cand_warm_approx); Costas keeps the exact one
+        // (its two stable points make the warm-up's branch matter, k_pll_reflip)
+        static const int approx = LDSP_KNOB("LDSP_PLL_WARM_APPROX", 1);
         hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s, pll_in(c), (long)c.n,
-                           c.st, c.gcur, cb, c.y, warm, c.costas);
+                           c.st, c.gcur, cb, c.y, warm, c.costas, (approx && !c.costas) ? 1 : 0);
     }
     LDSP_HIP(hipGetLastError());
     if (c.costas) {

@@ -184,7 +184,8 @@ struct SpecPlan {
     int H = 0;
     int tsa = 0;          // AGC small call: every chunk approximates from the true state up to its start
                           // (2: one wave, which also checks and repairs the chunks in order;
-                          // | 4: test hook, every chunk's start state 1 ulp off)
+                          // | 4: test hook, every chunk's start state 1 ulp off;
+                          // | 8: test hook, chunk-parallel call: odd chunks start 1 ulp off)
 };
 // scratch for iir_spec: chunk states + verifier flag words
 size_t spec_flags_offset(long nchunks, int ncomp, int fs);
@@ -198,7 +199,7 @@ struct AgcState {         // device-resident agc_crcf state
     int locked, mode;
     unsigned int timer, timeout;
     float threshold;
-    int pad[3];
+    int pad[3];           // test counters: [0] small-call in-kernel re-runs, [1] verifier re-runs, [2] runfix re-runs
 };
 constexpr int kAgcPow = 256;     // samples whose mean power sets a chunk's guessed gain
 void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hipStream_t s);

@@ -1036,6 +1036,7 @@ PYBIND11_MODULE(_liquiddsp, m)
     m.def("_debug_pll_margin", [](int lb) { return ldsp_debug_pll_margin(lb); });
     m.def("_profile_enable", [](bool on) { check(ldsp_profile_enable(on ? 1 : 0)); });
     m.def("_profile_reset", [] { check(ldsp_profile_reset()); });
+    m.def("_profile_only", [](const std::string& k) { check(ldsp_profile_only(k.c_str())); });
     m.def("_profile_report", [] {
         size_t len = 0;
         check(ldsp_profile_report(nullptr, 0, &len));
@@ -1242,6 +1243,15 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def_property_readonly("status", &AGC::status)
         .def("_tsa_perturb", [](AGC& a, bool on) { check(ldsp_debug_agc_tsa_perturb(a.q, on ? 1 : 0)); },
              "test hook: small calls re-run every chunk in-kernel (ldsp_debug_agc_tsa_perturb)")
+        .def("_perturb", [](AGC& a, bool on) { check(ldsp_debug_agc_perturb(a.q, on ? 1 : 0)); },
+             "test hook: chunk-parallel calls start every odd chunk 1 ulp off (ldsp_debug_agc_perturb)")
+        .def("_rounds", [](AGC& a, int r) { check(ldsp_debug_agc_rounds(a.q, r)); },
+             "test hook: repair rounds before the verifier (-1 default; ldsp_debug_agc_rounds)")
+        .def("_reruns", [](AGC& a) {
+            unsigned rf = 0, vf = 0;
+            check(ldsp_debug_agc_reruns(a.q, &rf, &vf));
+            return py::make_tuple(rf, vf);
+        }, "test hook: (repair-round, verifier) chunk re-runs since creation (ldsp_debug_agc_reruns)")
         .def("_tsa_reruns", [](AGC& a) {
             unsigned c = 0;
             check(ldsp_debug_agc_tsa_reruns(a.q, &c));

@@ -1,0 +1,57 @@
+#!/bin/bash
+# One parametrised GPU job (replaces the per-experiment gpu_rNN*.sh wrappers).
+#   bash scripts/gpu_job.sh TAG STEP [STEP ...]
+# Every step runs under its own time limit and writes gpurun_out/TAG/<step>.log;
+# the job stops at the first failing step (no GPU step runs after a failure).
+# Steps:
+#   pytest      the GPU test suite (one process)
+#   smoke       __graft_entry__.smoke()
+#   b20 / b100  bench.py at the driver setting (20 steps, 5 warm-up) / 100 steps, no components
+#   b20nk       the same 20 steps without per-kernel HIP events in the timed steps
+#   bench       bench.py with every component and the CPU baseline (the round-end line)
+#   tl20        tuning build, 20 steps, LDSP_PROF_TIMELINE dump + scripts/prof_timeline.py
+#   chains      scripts/chains_bench.py
+#   channels    scripts/channels_run.py (8 AMRadio chains on one GPU)
+#   c3spread    config-3 launch spread study (scripts/c3_spread.py)
+#   prof        rocprofv3 kernel stats + PMC passes (scripts/prof_round.sh TAG)
+#   py:<file>   python <file> (a one-off script under scripts/)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+tag=$1; shift
+o=gpurun_out/$tag
+mkdir -p "$o"
+export TMPDIR=/tmp
+B="python -u bench.py --no-cpu-baseline --no-components"
+run() {   # step name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$o/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc"
+  grep -E '^\{|passed|failed|error|smoke ok' "$o/$name.log" | tail -3 | cut -c1-400
+  [ $rc -eq 0 ] || { tail -15 "$o/$name.log"; exit $rc; }
+}
+for step in "$@"; do
+  case $step in
+    pytest) run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    b20) run b20 400 $B --steps 20 --warmup 5 ;;
+    b20nk) run b20nk 400 $B --steps 20 --warmup 5 --no-kprof ;;
+    b100) run b100 400 $B --steps 100 ;;
+    bench) run bench 900 python -u bench.py ;;
+    tl20) rm -f "$o/tl20.txt"
+          LDSP_PKG_DIR=build_tuning LDSP_PROF_TIMELINE="$o/tl20.txt" run tl20 400 $B --steps 20 --warmup 5
+          python scripts/prof_timeline.py "$o/tl20.txt" > "$o/tl20_summary.txt" 2>&1; tail -4 "$o/tl20_summary.txt" ;;
+    chains) run chains 400 python -u scripts/chains_bench.py ;;
+    channels) run channels 400 python -u scripts/channels_run.py ;;
+    c3spread) FIRBENCH_REPS=16 PMC_OUT="$o/c3" run c3pmc 600 bash scripts/fir_c3_pmc.sh
+              python scripts/c3_spread.py "$o/c3" > "$o/c3_spread.json"; head -c 1500 "$o/c3_spread.json"; echo ;;
+    prof) run prof 1100 bash scripts/prof_round.sh "$tag" ;;
+    py:*) f=${step#py:}; run "$(basename "$f" .py)" 600 python -u "$f" ;;
+    t20:*) kv=${step#t20:}; name="t20_$(echo "$kv" | tr ',=' '_-')"
+           env $(echo "$kv" | tr ',' ' ') LDSP_PKG_DIR=build_tuning \
+             timeout -k 10 400 $B --steps 20 --warmup 5 > "$o/$name.log" 2>&1
+           rc=$?; echo "[$name] rc=$rc"; grep '^{' "$o/$name.log" | cut -c1-330
+           grep -o '"single_stream_ms_per_step": [0-9.]*\|"k_pll_cand": {[^}]*}\|"k_agc_chunks": {[^}]*}\|"k_agc_runfix": {[^}]*}\|"k_pll_walk": {[^}]*}\|"repairs": [0-9]*' "$o/$name.log" | tr '\n' ' '; echo
+           [ $rc -eq 0 ] || { tail -15 "$o/$name.log"; exit $rc; } ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

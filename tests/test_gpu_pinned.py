@@ -130,3 +130,35 @@ def test_pool_limit_falls_back_to_pageable(ld):
     del held
     again = ld.bytes_to_iq(raw)                            # blocks back in the pool
     assert (_bits(again) == _bits(first)).all()
+
+
+def test_host_pools_bounded_under_thread_churn(ld, lib, rng):
+    # the staging pools of LDSP_MEM_HOST calls are per thread; a
+    # thread that exits hands its pool back (thread_local holder), so 40
+    # short-lived threads making host calls one after another reuse one pool
+    # instead of each leaking 2 x 16 MB of page-locked memory.
+    import threading
+    x = (rng.standard_normal(1 << 16) + 1j * rng.standard_normal(1 << 16)).astype(np.complex64)
+    f = ld.ComplexFIRFilter(np.float32([0.5, 0.25, 0.125]))
+    f.mode = "exact"
+    total0, idle0 = C.c_size_t(0), C.c_size_t(0)
+    assert lib.ldsp_debug_host_pools(C.byref(total0), C.byref(idle0)) == 0
+    outs = []
+
+    def work():
+        outs.append(f(x))
+
+    for _ in range(40):
+        t = threading.Thread(target=work)
+        t.start()
+        t.join()
+    total, idle = C.c_size_t(0), C.c_size_t(0)
+    assert lib.ldsp_debug_host_pools(C.byref(total), C.byref(idle)) == 0
+    assert len(outs) == 40
+    assert total.value <= total0.value + 1, (total0.value, total.value)
+    assert idle.value >= 1
+    # the calls still carried the filter state across threads in order
+    ref = ld.ComplexFIRFilter(np.float32([0.5, 0.25, 0.125]))
+    ref.mode = "exact"
+    for i in range(40):
+        assert np.array_equal(_bits(outs[i]), _bits(ref(x)))
