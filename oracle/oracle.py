@@ -170,6 +170,7 @@ VARIANTS = {
     "libm": "libliquid_restate_libm.so",
     "simd": "libliquid_restate_simd.so",
     "libm_simd": "libliquid_restate_libm_simd.so",
+    "asan": "libliquid_restate_asan.so",          # make -C oracle asan (tests/test_sanitizers.py)
 }
 _variant_mods = {}
 

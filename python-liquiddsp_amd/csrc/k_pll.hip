@@ -773,63 +773,76 @@ struct WState {
     uint32_t Kb, D, nrep, nfb, nlb, nsame;
 };
 
-// Generic walk of every sample in [sa, sb]: 64 consecutive samples per step
-// (records, offset model and loop inputs loaded one step ahead), each repair
-// evaluated in full at the true index (table in LDS) against the candidate's
-// recorded kicks, its output written to y, the offsets of the later lanes
-// updated in place.  Used where the sparse walk cannot prove a gap
-// clean, and for every lane-block in the LDSP_DEBUG_PLL=2 check.
-struct FbGroup {
-    uint4 r0;             // candidate record (w, k1, k2, out)
-    uint32_t A;
-    float2 u0, u1;
-};
-__device__ __forceinline__ FbGroup fb_load(long base, long sb, const CandBuf& cb, const FullCtx& fc, int lane)
-{
-    FbGroup q;
-    const long s = min(base + lane, sb);
-    q.r0 = cb.rec[s];
-    const long k = s / kCand;
-    q.A = cb.pth[k] + (uint32_t)s * cb.pd[k];
-    q.u0 = fc.x0[s];
-    const long g = s - fc.m;
-    q.u1 = g >= 0 ? fc.x[g] : fc.hist[g + fc.m];
-    return q;
-}
+// Generic walk of every sample in [sa, sb] (the samples of one lane-block's
+// entries and the gaps between them): 64 consecutive samples per step, the
+// candidate phases and offset model of up to kFbPre steps loaded up front (one
+// memory round trip for a whole lane-block's range instead of one per step),
+// each repair applied at the true index.  A repair at one of the lane-block's
+// entries that crosses the one cell its entry record allows (E1) takes that
+// record's kick differences and output (the same pll_eval k_pll_entries ran);
+// any other one (a gap sample, or two or more cells) loads its loop inputs and
+// evaluates the loop step in full against the candidate's recorded kicks.  Used
+// where the sparse walk cannot prove a gap clean, and for every lane-block in
+// the LDSP_DEBUG_PLL=2 check (which evaluates every repair in full).
+constexpr int kFbPre = 16;
 
 __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_t S, CandBuf cb, FullCtx fc,
-                                             const float* tab, float* y, int lane)
+                                             const float* tab, float* y, int lane, uint32_t esrel, uint32_t edk1,
+                                             uint32_t edk2p, uint32_t eout, int nv)
 {
-    FbGroup nx = fb_load(sa, sb, cb, fc, lane);
-    for (long base = sa; base <= sb; base += 64) {
-        const FbGroup q = nx;
-        if (base + 64 <= sb) nx = fb_load(base + 64, sb, cb, fc, lane);
-        const unsigned long long M = __builtin_amdgcn_ballot_w64(base + lane <= sb);
-        const uint32_t u = q.r0.x & 0x3fffffu, srel = (uint32_t)(base + lane - (long)S);
-        uint32_t v = u + g.Kb + srel * g.D + q.A;
-        unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
-        while (mask != 0) {
-            const int j = __builtin_ctzll(mask);
-            const uint32_t vj = rl(v, j);
-            // the loop step at the true index (any number of cells from the
-            // candidate's), evaluated in full; the candidate's kicks from its record
-            const uint32_t ic = rl(q.r0.x, j) >> 22;
-            const float2 u0 = make_float2(__uint_as_float(rl(__float_as_uint(q.u0.x), j)),
-                                          __uint_as_float(rl(__float_as_uint(q.u0.y), j)));
-            const float2 u1 = make_float2(__uint_as_float(rl(__float_as_uint(q.u1.x), j)),
-                                          __uint_as_float(rl(__float_as_uint(q.u1.y), j)));
-            const Kick kt = pll_eval(tab, (ic + (vj >> 22)) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index,
-                                     fc.costas, fc.out_idx);
-            const uint32_t dk1 = rfl(kt.k1 - rl(q.r0.y, j));
-            const uint32_t dk2 = rfl(kt.k2 - rl(q.r0.z, j));
-            const uint32_t out = rfl(__float_as_uint(kt.out));
-            const uint32_t rrel = (uint32_t)j + (uint32_t)(base - (long)S);
-            if (lane == 0) y[base + j] = __uint_as_float(out);
-            g.Kb += dk2 - rrel * dk1;
-            g.D += dk1;
-            g.nrep++;
-            v += dk2 + (srel - rrel) * dk1;
-            mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M & ((~0ull << j) << 1);
+    const unsigned long long emask = nv >= 64 ? ~0ull : nv <= 0 ? 0ull : ((1ull << nv) - 1ull);
+    const bool use_e1 = cb.dbg != 2;
+    const uint32_t* recw = (const uint32_t*)cb.rec;          // word 0 of record s: recw[4 s]
+    for (long b0 = sa; b0 <= sb; b0 += 64l * kFbPre) {
+        uint32_t W[kFbPre], A[kFbPre];
+#pragma unroll
+        for (int q = 0; q < kFbPre; q++) {
+            const long s = min(b0 + 64l * q + lane, sb);
+            W[q] = recw[4 * s];
+            const long k = s / kCand;
+            A[q] = cb.pth[k] + (uint32_t)s * cb.pd[k];
+        }
+#pragma unroll
+        for (int q = 0; q < kFbPre; q++) {
+            const long base = b0 + 64l * q;
+            if (base > sb) break;
+            const unsigned long long M = __builtin_amdgcn_ballot_w64(base + lane <= sb);
+            const uint32_t srel = (uint32_t)(base + lane - (long)S);
+            uint32_t v = (W[q] & 0x3fffffu) + g.Kb + srel * g.D + A[q];
+            unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
+            while (mask != 0) {
+                const int j = __builtin_ctzll(mask);
+                const uint32_t vj = rl(v, j), wj = rl(W[q], j);
+                const uint32_t rrel = (uint32_t)j + (uint32_t)(base - (long)S);
+                const uint32_t cell = vj >> 22;            // true index - candidate's (mod 1024)
+                const unsigned long long em = __builtin_amdgcn_ballot_w64(esrel == rrel) & emask;
+                uint32_t dk1, dk2p, out;
+                if (use_e1 && em != 0 && cell == ((wj & 0x3fffffu) >= (1u << 21) ? 1u : 1023u)) {
+                    const int L = __builtin_ctzll(em);
+                    dk1 = rl(edk1, L);
+                    dk2p = rl(edk2p, L);                  // dk2 - srel dk1
+                    out = rl(eout, L);
+                } else {
+                    // the loop step at the true index (any number of cells from the
+                    // candidate's), evaluated in full; the candidate's kicks from its record
+                    const long s = base + j;
+                    const uint4 r0 = cb.rec[s];
+                    const float2 u0 = fc.x0[s];
+                    const long gi = s - fc.m;
+                    const float2 u1 = gi >= 0 ? fc.x[gi] : fc.hist[gi + fc.m];
+                    const Kick kt = pll_eval(tab, ((wj >> 22) + cell) & 0x3ffu, u0, u1, fc.alpha, fc.beta,
+                                             fc.mod_index, fc.costas, fc.out_idx);
+                    dk1 = rfl(kt.k1 - r0.y);
+                    dk2p = rfl(kt.k2 - r0.z) - rrel * dk1;
+                    out = rfl(__float_as_uint(kt.out));
+                }
+                if (lane == 0) y[base + j] = __uint_as_float(out);
+                g.Kb += dk2p;
+                g.D += dk1;
+                g.nrep++;
+                v += dk2p + srel * dk1;
+                mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M & ((~0ull << j) << 1);
+            }
         }
     }
     return g;
@@ -916,7 +929,8 @@ __device__ __forceinline__ void walk_lb(const uint4& E0, const uint4& E1, int nv
             WState r = g0;
             r.nfb++;
             const long s_first = prev.first ? 0l : (long)prev.S + rl(prev.srel, prev.nv - 1) + 1;
-            r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, tab, y, lane);
+            r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, tab, y, lane, E0.z, E1.x, E1.y,
+                              E1.z, nv);
             g.Kb = rfl(r.Kb);
             g.D = rfl(r.D);
             g.nrep = rfl(r.nrep);
@@ -1075,7 +1089,8 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         r.nrep -= nr;
         r.nfb++;
         const long s_first = prev.first ? 0l : (long)prev.S + rl(prev.srel, prev.nv - 1) + 1;
-        r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, tab, y, lane);
+        r = walk_fallback(r, s_first, (long)S + rl(srel, nv - 1), S, cb, fc, tab, y, lane, E0.z, E1.x, E1.y, E1.z,
+                          nv);
         g.Kb = rfl(r.Kb);
         g.D = rfl(r.D);
         g.nrep = rfl(r.nrep);
@@ -1407,6 +1422,9 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
     uint32_t S = 0;
     PrevLB prev{0u, 1, 0u, true};
     unsigned long long cyc_walk = 0, cyc_wait = 0;
+#ifdef LDSP_TUNING
+    unsigned long long cyc_undo = 0, cyc_fb = 0;      // product loop's block redos: undo pass, fallback lane-blocks
+#endif
     static_assert(VAR == 0 || VAR == 32 || VAR == 64 || VAR == 96, "walker variant");
     if constexpr (F24 && !STATS) {
         // the product path: the block loop in one asm statement (walk_asm_loop)
@@ -1436,6 +1454,9 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
 #endif
                 if (w.c > c0) prev = PrevLB{w.s7, 64, w.Sprev, false};
                 if (w.c >= (uint32_t)nblk) break;
+#ifdef LDSP_TUNING
+                const unsigned long long tf0 = wall_clock64();      // fallback cost (stats[2], stats[3])
+#endif
                 // block c failed its interval test: undo its speculative stores (the
                 // candidates' outputs at every entry), then redo it lane-block by
                 // lane-block from its entry state (each rewrite lands after the previous one)
@@ -1445,11 +1466,24 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 S = w.S;
                 float* yb = y + S;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                for (int q = 0; q < kBlkE / 64; q++) {
-                    const uint32_t sr = b.e[0][q * 64 + lane].z;
-                    if (q * 64 + lane < cnt) y[S + sr] = __uint_as_float(cb.rec[(long)S + sr].w);
+                {
+                    // every load first (one round trip), then the stores
+                    const uint32_t* recw = (const uint32_t*)cb.rec;
+                    uint32_t sr[kBlkE / 64], cw[kBlkE / 64];
+#pragma unroll
+                    for (int q = 0; q < kBlkE / 64; q++) {
+                        sr[q] = b.e[0][q * 64 + lane].z;
+                        cw[q] = recw[4 * ((long)S + (q * 64 + lane < cnt ? sr[q] : 0u)) + 3];
+                    }
+#pragma unroll
+                    for (int q = 0; q < kBlkE / 64; q++)
+                        if (q * 64 + lane < cnt) y[S + sr[q]] = __uint_as_float(cw[q]);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef LDSP_TUNING
+                const unsigned long long tu1 = wall_clock64();
+                cyc_undo += tu1 - tf0;
+#endif
                 g.Kb = w.kb0;
                 g.D = w.d0;
                 g.nrep = w.nrep0;
@@ -1458,8 +1492,15 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                     const uint4 N0 = b.e[0][min(q + 1, kBlkE / 64 - 1) * 64 + lane];
                     uint32_t x = C0.x + g.Kb + C0.z * g.D;
                     unsigned long long mk = __builtin_amdgcn_ballot_w64(x > C0.y);
+#ifdef LDSP_TUNING
+                    const unsigned long long tq0 = wall_clock64();
+                    const uint32_t nfb0 = g.nfb;
+#endif
                     walk_lb24<false>(C0, C1, min(64, cnt - q * 64), g, S, prev, cb, fc, wtab, y, lane, x, mk, N0.x,
                                      N0.z, N0.y, yb);
+#ifdef LDSP_TUNING
+                    if (g.nfb != nfb0) cyc_fb += wall_clock64() - tq0;
+#endif
                 }
                 w.kb = rfl(g.Kb);
                 w.d = rfl(g.D);
@@ -1468,6 +1509,10 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 w.c++;
+#ifdef LDSP_TUNING
+                cyc_walk += wall_clock64() - tf0;
+                cyc_wait++;
+#endif
             }
             g.Kb = w.kb;
             g.D = w.d;
@@ -1543,6 +1588,12 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         cb.stats[0] = g.nrep;
         cb.stats[1] = g.nfb;
         cb.stats[4] = NE;
+#ifdef LDSP_TUNING
+        if (F24 && !STATS) {             // product loop: 10 ns ticks in fallback block redos; their count
+            cb.stats[2] = cyc_walk;      // | undo ticks << 16 | fallback lane-block ticks << 40
+            cb.stats[3] = cyc_wait | (min(cyc_undo, 0xffffffull) << 16) | (min(cyc_fb, 0xffffffull) << 40);
+        }
+#endif
         if (STATS) {
             cb.stats[2] = cyc_walk;
             cb.stats[3] = cyc_wait;

@@ -32,20 +32,24 @@ run() {   # step name, seconds, command...
 for step in "$@"; do
   case $step in
     pytest) run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    pytest:*) k=${step#pytest:}; run "pytest_$k" 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$k" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     b20) run b20 400 $B --steps 20 --warmup 5 ;;
     b20nk) run b20nk 400 $B --steps 20 --warmup 5 --no-kprof ;;
     b100) run b100 400 $B --steps 100 ;;
     bench) run bench 900 python -u bench.py ;;
-    tl20) rm -f "$o/tl20.txt"
-          LDSP_PKG_DIR=build_tuning LDSP_PROF_TIMELINE="$o/tl20.txt" run tl20 400 $B --steps 20 --warmup 5
-          python scripts/prof_timeline.py "$o/tl20.txt" > "$o/tl20_summary.txt" 2>&1; tail -4 "$o/tl20_summary.txt" ;;
+    tl20|tl20:*) kv=${step#tl20}; kv=${kv#:}; name="tl20$(echo "_$kv" | tr ',=' '_-')"; rm -f "$o/$name.txt"
+          env $(echo "$kv" | tr ',' ' ') LDSP_PKG_DIR=build_tuning LDSP_PROF_TIMELINE="$o/$name.txt" \
+            timeout -k 10 400 $B --steps 20 --warmup 5 --no-kprof > "$o/$name.log" 2>&1
+          rc=$?; echo "[$name] rc=$rc"; grep '^{' "$o/$name.log" | cut -c1-330; [ $rc -eq 0 ] || exit $rc
+          python scripts/prof_timeline.py "$o/$name.txt" > "$o/${name}_summary.txt" 2>&1; head -3 "$o/${name}_summary.txt"; tail -1 "$o/${name}_summary.txt" ;;
     chains) run chains 400 python -u scripts/chains_bench.py ;;
     channels) run channels 400 python -u scripts/channels_run.py ;;
     c3spread) FIRBENCH_REPS=16 PMC_OUT="$o/c3" run c3pmc 600 bash scripts/fir_c3_pmc.sh
               python scripts/c3_spread.py "$o/c3" > "$o/c3_spread.json"; head -c 1500 "$o/c3_spread.json"; echo ;;
     prof) run prof 1100 bash scripts/prof_round.sh "$tag" ;;
     py:*) f=${step#py:}; run "$(basename "$f" .py)" 600 python -u "$f" ;;
+    tpy:*) f=${step#tpy:}; LDSP_PKG_DIR=build_tuning run "t_$(basename "$f" .py)" 600 python -u "$f" ;;
     t20:*) kv=${step#t20:}; name="t20_$(echo "$kv" | tr ',=' '_-')"
            env $(echo "$kv" | tr ',' ' ') LDSP_PKG_DIR=build_tuning \
              timeout -k 10 400 $B --steps 20 --warmup 5 > "$o/$name.log" 2>&1
