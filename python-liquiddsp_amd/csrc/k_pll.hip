@@ -1142,7 +1142,38 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     "s_add_u32 %[kb], %[kb], %[dk2]\n\t"                                                                   \
     "s_add_u32 %[d], %[d], %[dk1]\n\t"                                                                     \
     "v_cmp_gt_u32_e32 vcc, " X ", " W "\n\t"
+// The lane-block transition: the next lane-block's offsets (v_mul_lo, quarter
+// rate, then v_add3) are the critical path into its VCCZ branch, so the
+// independent work -- this lane-block's repaired mask, store offset and interval
+// test -- is issued between the multiply and the add and the store between the
+// add and the compare, instead of after them (in-order issue: an instruction
+// waiting on a result holds every later one).
 #define WL_LB(E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, SXN, X, XN, TAIL)                           \
+    "s_cbranch_vccz 2f\n"                                                                                  \
+    "1:\n\t"                                                                                               \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
+    WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccnz 1b\n"                                                    \
+    "3:\n\t"                                                                                               \
+    "s_mov_b64 exec, -1\n"                                                                                 \
+    "2:\n\t"                                                                                               \
+    "v_mul_lo_u32 %[t2], %[d], " SXN "\n\t"                                                                \
+    "v_cmp_gt_u32_e64 %[pm], " X ", " E0Y "\n\t"                                                           \
+    "v_lshl_add_u32 %[off], " E0Z ", 2, %[s4]\n\t"                                                         \
+    "v_sub_u32 %[t], " X ", " E0W "\n\t"                                                                   \
+    "v_sub_u32_e64 %[t], %[t], " E1W " clamp\n\t"                                                          \
+    "v_add3_u32 " XN ", " N0X ", %[kb], %[t2]\n\t"                                                         \
+    "s_mov_b64 exec, %[pm]\n\t"                                                                            \
+    "global_store_dword %[off], " E1Z ", %[yb]\n\t"                                                        \
+    "v_or_b32 %[acc], %[acc], %[t]\n\t"                                                                    \
+    "s_mov_b64 exec, -1\n\t"                                                                               \
+    "v_cmp_gt_u32_e32 vcc, " XN ", " N0Y "\n\t"                                                            \
+    "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
+    "s_add_u32 %[nrep], %[nrep], %[nr]\n\t" TAIL
+#ifdef LDSP_TUNING
+// Round 4's lane-block order (timing A/B against WL_LB: k_pll_walk VAR 128)
+#define WL_LB_ORIG(E0X, E0Y, E0Z, E0W, E1X, E1Y, E1Z, E1W, N0X, N0Y, SXN, X, XN, TAIL)                           \
     "s_cbranch_vccz 2f\n"                                                                                  \
     "1:\n\t"                                                                                               \
     WX_REP(E1X, E1Y, E0Z, E0Y, X) "s_cbranch_vccz 3f\n\t"                                                  \
@@ -1165,7 +1196,6 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
     "s_mov_b64 exec, -1\n\t"                                                                               \
     "s_bcnt1_i32_b64 %[nr], %[pm]\n\t"                                                                     \
     "s_add_u32 %[nrep], %[nrep], %[nr]\n\t" TAIL
-#ifdef LDSP_TUNING
 // Timing variants of the product loop (tuning build, k_pll_walk VAR 32 / 64; wrong
 // outputs): NOREP skips every repair loop (the lane-block transitions, stores and
 // tests alone), NOST drops the store / interval test / repair count (loop + transitions).
@@ -1305,7 +1335,7 @@ __device__ __forceinline__ void walk_lb24(const uint4& E0, const uint4& E1, int 
         "s_cbranch_scc1 9b\n"                                                                                         \
         "8:\n\t"                                                                                                      \
         "s_waitcnt lgkmcnt(0)"                                                                                        \
-        : [xa] "=&v"(xa), [xb] "=&v"(xb), [t] "=&v"(t), [off] "=&v"(off), [acc] "=&v"(acc),                           \
+        : [xa] "=&v"(xa), [xb] "=&v"(xb), [t] "=&v"(t), [t2] "=&v"(t2), [off] "=&v"(off), [acc] "=&v"(acc),          \
           [sx7] "=&v"(sx7), [ln] "=&v"(ln), [lh] "=&v"(lh), [s7] "+v"(s7),                                            \
           [pm] "=&s"(pm), [bad] "=&s"(bad),                                                                           \
           [kb] "+s"(kb), [d] "+s"(d), [nrep] "+s"(nrep), [c] "+s"(c), [S] "+s"(S), [Sp] "+s"(Sprev),                  \
@@ -1341,7 +1371,7 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
     const uint32_t rend = ring + kRing * kSlot;
     const uint32_t la = ring + (w.c % kRing) * kSlot + lane16;        // block c's entries (prologue)
     uint32_t sn = ring + ((w.c + 1) % kRing) * kSlot;                  // slot of block c + 1
-    uint32_t xa, xb, t, off, acc, sx7, ln, lh, s7 = w.s7;
+    uint32_t xa, xb, t, t2, off, acc, sx7, ln, lh, s7 = w.s7;
     uint32_t j, dk1, dk2, nr, snx, dS, tS, s4;
     unsigned long long pm, bad;
     uint32_t kb = w.kb, d = w.d, nrep = w.nrep, c = w.c, S = w.S, Sprev = w.Sprev, kb0, d0, nrep0;
@@ -1353,6 +1383,8 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
         WALK_ASM(WL_LB_NOREP);
     } else if constexpr (PV == 2) {
         WALK_ASM(WL_LB_NOST);
+    } else if constexpr (PV == 4) {
+        WALK_ASM(WL_LB_ORIG);
     } else {
         WALK_ASM(WL_LB_HELPER);
     }
@@ -1425,7 +1457,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
 #ifdef LDSP_TUNING
     unsigned long long cyc_undo = 0, cyc_fb = 0;      // product loop's block redos: undo pass, fallback lane-blocks
 #endif
-    static_assert(VAR == 0 || VAR == 32 || VAR == 64 || VAR == 96, "walker variant");
+    static_assert(VAR == 0 || VAR == 32 || VAR == 64 || VAR == 96 || VAR == 128, "walker variant");
     if constexpr (F24 && !STATS) {
         // the product path: the block loop in one asm statement (walk_asm_loop)
         if (wave != 0) {
@@ -1801,7 +1833,7 @@ void pll_back(const PllCall& c, hipStream_t s)
             if (!stats && var > 0) {
 #define WALK_VAR(V) case V: hipLaunchKernelGGL((k_pll_walk<true, false, V>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y); break;
                 switch (var) {
-                WALK_VAR(32) WALK_VAR(64) WALK_VAR(96)
+                WALK_VAR(32) WALK_VAR(64) WALK_VAR(96) WALK_VAR(128)
                 default: break;
                 }
 #undef WALK_VAR

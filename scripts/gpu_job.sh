@@ -49,7 +49,10 @@ for step in "$@"; do
               python scripts/c3_spread.py "$o/c3" > "$o/c3_spread.json"; head -c 1500 "$o/c3_spread.json"; echo ;;
     prof) run prof 1100 bash scripts/prof_round.sh "$tag" ;;
     py:*) f=${step#py:}; run "$(basename "$f" .py)" 600 python -u "$f" ;;
-    tpy:*) f=${step#tpy:}; LDSP_PKG_DIR=build_tuning run "t_$(basename "$f" .py)" 600 python -u "$f" ;;
+    tpy:*) f=${step#tpy:}; kv=""; case $f in *:*) kv=${f#*:}; f=${f%%:*};; esac
+           name="t_$(basename "$f" .py)$(echo "${kv:+_$kv}" | tr ',=' '_-')"
+           env $(echo "$kv" | tr ',' ' ') LDSP_PKG_DIR=build_tuning timeout -k 10 600 python -u "$f" > "$o/$name.log" 2>&1
+           rc=$?; echo "[$name] rc=$rc"; grep '^{' "$o/$name.log" | cut -c1-400; [ $rc -eq 0 ] || { tail -15 "$o/$name.log"; exit $rc; } ;;
     t20:*) kv=${step#t20:}; name="t20_$(echo "$kv" | tr ',=' '_-')"
            env $(echo "$kv" | tr ',' ' ') LDSP_PKG_DIR=build_tuning \
              timeout -k 10 400 $B --steps 20 --warmup 5 > "$o/$name.log" 2>&1
