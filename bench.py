@@ -593,6 +593,9 @@ def components(L, device, reps=5):
     strm = [[torch.cuda.Stream(device) for _ in range(2)] for _ in range(8)]
     out["channels_per_gpu"] = multi_channel(L, device, fused=True, strm=strm)
     out["channels_per_gpu_unfused"] = multi_channel(L, device, strm=strm)
+    bs = [torch.cuda.Stream(device) for _ in range(3)]
+    out["channels_per_gpu_batched"] = multi_channel_batched(L, device, 8, strm=bs)
+    out["channels_per_gpu_batched_16"] = multi_channel_batched(L, device, 16, n=32 << 20, strm=bs)
     return out
 
 
@@ -619,6 +622,31 @@ def exact_chain(L, device, n):
     del x
     return {"ms_per_step": round(el * 1e3, 2), "Msamples_s": round(n / el / 1e6, 2), "kernels_ms": kern,
             "iir_kernel": "k_iir_pipe", "note": "exact (bit-identical) mode: the IIR is one sequential recursion"}
+
+
+def multi_channel_batched(L, device, channels=8, steps=10, n=64 << 20, per=3, strm=None):
+    """The same C channels stepped with the many-calls (liquiddsp.filter_resample_many /
+    execute_many): one kernel launch per stage for all channels, each step on one of
+    `per` rotating streams (steps overlap: step k+1's filters run under step k's walks).
+    Same bits per channel as the per-channel calls (tests/test_gpu_many.py)."""
+    xs = [synth_channel(n, r % 8, device) for r in range(channels)]
+    radios = [AMRadio(L) for _ in range(channels)]
+    if strm is None:
+        strm = [torch.cuda.Stream(device) for _ in range(per)]
+    iirs, rss = [r.bandpass for r in radios], [r.resample for r in radios]
+    agcs, ams, des = [r.agc for r in radios], [r.am for r in radios], [r.audio_filter for r in radios]
+
+    def step(k, w=None):
+        kk = k if k is not None else w
+        with torch.cuda.stream(strm[kk % len(strm)]):
+            a = L.filter_resample_many(iirs, rss, xs)
+            L.execute_many(des, L.execute_many(ams, L.execute_many(agcs, a)))
+
+    t = timed_steps(step, steps, max(2, len(strm)), torch.cuda.synchronize, lambda: None)
+    del xs
+    return {"channels": channels, "batched": True, "streams": len(strm), "steps": steps,
+            "ms_per_step": round(t / steps * 1e3, 3), "Msamples_s": round(channels * n * steps / t / 1e6, 1),
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")}
 
 
 def multi_channel(L, device, channels=8, steps=10, n=64 << 20, per=2, split=False, fused=False, strm=None,

@@ -410,6 +410,25 @@ int ldsp_delay_execute(ldsp_delay_t q, const void *x, size_t n, int cplx, void *
  * ---------------------------------------------------------------------- */
 int ldsp_bytes_to_iq(const void *in, size_t nbytes, void *y, int mem, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Many-calls: one call each on C independent objects of one class (no
+ * reference counterpart -- the reference's SDR callback runs one channel's
+ * chain per call, README.md:53-58; SURVEY 7 H5 / 8(e): channels batched on one
+ * GPU).  Equivalent to calling the single-object execute on q[0], .., q[C-1]
+ * in turn on `stream`, bit for bit, but every kernel runs as ONE launch for
+ * all objects that take the same path (blockIdx.y = object), so a step of C
+ * channels issues as many launches as one channel's.  Device pointers only;
+ * all objects get n input samples; the objects must be distinct.
+ * iirfilt_resamp: nout[c] receives object c's output count (cap per object).
+ * ---------------------------------------------------------------------- */
+int ldsp_agc_execute_many(ldsp_agc_t *q, const void *const *x, size_t n, void *const *y, int C, void *stream);
+int ldsp_ampmodem_demodulate_many(ldsp_ampmodem_t *q, const void *const *x, size_t n, void *const *y, int C,
+                                  void *stream);
+int ldsp_iirfilt_execute_many(ldsp_iirfilt_t *q, const void *const *x, size_t n, void *const *y, int C,
+                              void *stream);
+int ldsp_iirfilt_resamp_execute_many(ldsp_iirfilt_t *q, ldsp_resamp_t *rs, const void *const *x, size_t n,
+                                     void *const *y, size_t cap, size_t *nout, int C, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

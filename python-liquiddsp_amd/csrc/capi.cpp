@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "batch.hpp"
 #include "design.hpp"
 #include "modal.hpp"
 #include "kernels.hpp"
@@ -1094,6 +1095,9 @@ std::string g_only_name;
 
 Scope::Scope(hipStream_t s_, const char* n) : s(s_), name(n)
 {
+    // a launcher that issues its kernel directly while a many-call records (batch.hpp)
+    // would run it out of order: refuse before the launch
+    if (batch_active()) throw Error(LDSP_EUNSUP, std::string("kernel not batchable in a many-call: ") + n);
     if (!enabled()) return;
     const char* only = g_only.load(std::memory_order_relaxed);
     if (only && std::strcmp(only, n) != 0) return;
@@ -2897,6 +2901,78 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
         q->ord.mark(e.stream);
         q->last = e.stream;
         q->stg.finish(e, y, 2 * k * 4);
+    });
+}
+
+// ------------------------------------------------------- many-calls (batch.hpp)
+// C independent objects of one class, one call each on the same stream, with
+// one launch per kernel for all of them: every object's execute runs with the
+// recorder active (its host bookkeeping exactly as for a single call), then the
+// recorded work is issued with the launches of objects that run the same
+// kernel on the same grid merged (blockIdx.y = object).  Device memory only;
+// the objects must be distinct.
+extern "C++" {
+template <class T, class F>
+static int run_many(T* const* q, int C, void* stream, F&& one)
+{
+    return guard([&] {
+        LDSP_REQUIRE(q != nullptr && C >= 1 && C <= 4096, "many: 1 .. 4096 objects");
+        for (int c = 0; c < C; c++) {
+            LDSP_REQUIRE(q[c] != nullptr, "many: NULL object");
+            for (int c2 = 0; c2 < c; c2++) LDSP_REQUIRE(q[c2] != q[c], "many: the objects must be distinct");
+        }
+        BatchRecorder rec(C, (hipStream_t)stream);
+        int rc = LDSP_OK;
+        std::string err;
+        for (int c = 0; c < C && rc == LDSP_OK; c++) {
+            rec.channel(c);
+            rc = one(c);
+            if (rc != LDSP_OK) err = g_last_error;
+        }
+        rec.flush();                         // every object whose host state advanced gets its device work
+        if (rc != LDSP_OK) throw Error(rc, err);
+    });
+}
+} // extern "C++"
+
+int ldsp_agc_execute_many(ldsp_agc_t* q, const void* const* x, size_t n, void* const* y, int C, void* stream)
+{
+    LDSP_RANGE("ldsp_agc_execute_many");
+    return run_many(q, C, stream, [&](int c) {
+        return ldsp_agc_execute(q[c], x[c], n, y[c], nullptr, LDSP_MEM_DEVICE, stream);
+    });
+}
+
+int ldsp_ampmodem_demodulate_many(ldsp_ampmodem_t* q, const void* const* x, size_t n, void* const* y, int C,
+                                  void* stream)
+{
+    LDSP_RANGE("ldsp_ampmodem_demodulate_many");
+    return run_many(q, C, stream, [&](int c) {
+        return ldsp_ampmodem_demodulate(q[c], x[c], n, y[c], LDSP_MEM_DEVICE, stream);
+    });
+}
+
+int ldsp_iirfilt_execute_many(ldsp_iirfilt_t* q, const void* const* x, size_t n, void* const* y, int C, void* stream)
+{
+    LDSP_RANGE("ldsp_iirfilt_execute_many");
+    return run_many(q, C, stream, [&](int c) {
+        return ldsp_iirfilt_execute(q[c], x[c], n, y[c], LDSP_MEM_DEVICE, stream);
+    });
+}
+
+int ldsp_iirfilt_resamp_execute_many(ldsp_iirfilt_t* q, ldsp_resamp_t* rs, const void* const* x, size_t n,
+                                     void* const* y, size_t cap, size_t* nout, int C, void* stream)
+{
+    LDSP_RANGE("ldsp_iirfilt_resamp_execute_many");
+    for (int c = 0; c < C; c++)                  // the resamplers must be distinct too
+        for (int c2 = 0; c2 < c; c2++)
+            if (rs && rs[c] == rs[c2]) {
+                set_last_error("many: the objects must be distinct");
+                return LDSP_EINVAL;
+            }
+    return run_many(q, C, stream, [&](int c) {
+        return ldsp_iirfilt_resamp_execute(q[c], rs[c], x[c], n, y[c], cap, nout ? nout + c : nullptr,
+                                           LDSP_MEM_DEVICE, stream);
     });
 }
 

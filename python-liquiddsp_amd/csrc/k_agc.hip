@@ -12,6 +12,7 @@
 // (k_agc_runfix), and a single-wave verifier re-checks every chunk and re-runs
 // any leftover, so the output is always identical to the sequential evaluation.
 // (The AmpModem PLL lives in k_pll.hip.)
+#include "batch.hpp"
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 #include "ldsp_math.hpp"
@@ -196,7 +197,7 @@ __device__ __forceinline__ void agc_run(AgcReg& r, const AgcState& p, const X& x
 
 // One lane runs the loop; the wave stages the input through LDS 2048 samples
 // at a time so the loop never waits on a global load.
-__global__ void __launch_bounds__(64) k_agc_seq(const float2* __restrict__ x, long n, AgcState* st,
+__device__ __forceinline__ void k_agc_seq_body(const float2* __restrict__ x, long n, AgcState* st,
                                                 float2* __restrict__ y, uint8_t* __restrict__ status)
 {
     LDSP_LATENCY_CRITICAL();
@@ -218,6 +219,16 @@ __global__ void __launch_bounds__(64) k_agc_seq(const float2* __restrict__ x, lo
         st->timer = r.timer;
     }
 }
+struct AgcSeqArgs {
+    const float2* x;
+    long n;
+    AgcState* st;
+    float2* y;
+    uint8_t* status;
+};
+__device__ __forceinline__ void k_agc_seq_run(const AgcSeqArgs& a) { k_agc_seq_body(a.x, a.n, a.st, a.y, a.status); }
+LDSP_KERNEL_PAIR(k_agc_seq, AgcSeqArgs, k_agc_seq_run, 64)
+
 
 // scratch: [nchunks][2 (start, end)][4 words: g, y2p, mode, timer]
 // Chunk k's exact run starts W samples early (w0 = s0 - W) from a guessed
@@ -232,7 +243,7 @@ constexpr int kPow = kAgcPow;
 // chunk, chunk 0 included, starts from a guess (H >= W + Wa + kPow), so the
 // kernel never reads the true state and may overlap the previous call's
 // back half; chunk 0 is then checked against the true state like any other.
-__global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x, const float2* __restrict__ hist, long H,
+__device__ __forceinline__ void k_agc_chunks_body(const float2* __restrict__ x, const float2* __restrict__ hist, long H,
                                                    long n, const AgcState* st, int C, int W, int Wa, long nch,
                                                    unsigned* __restrict__ sc, float2* __restrict__ y,
                                                    uint8_t* __restrict__ status, int tsa)
@@ -349,6 +360,24 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
     gs[6] = (unsigned)r.mode;
     gs[7] = r.timer;
 }
+struct AgcChunksArgs {
+    const float2* x;
+    const float2* hist;
+    long H;
+    long n;
+    const AgcState* st;
+    int C;
+    int W;
+    int Wa;
+    long nch;
+    unsigned* sc;
+    float2* y;
+    uint8_t* status;
+    int tsa;
+};
+__device__ __forceinline__ void k_agc_chunks_run(const AgcChunksArgs& a) { k_agc_chunks_body(a.x, a.hist, a.H, a.n, a.st, a.C, a.W, a.Wa, a.nch, a.sc, a.y, a.status, a.tsa); }
+LDSP_KERNEL_PAIR(k_agc_chunks, AgcChunksArgs, k_agc_chunks_run, 64)
+
 
 // One-wave small call (tsa 2) with the call's input staged in LDS first: the
 // approximate loop of every lane runs up to its chunk's start over the same
@@ -356,7 +385,7 @@ __global__ void __launch_bounds__(64) k_agc_chunks(const float2* __restrict__ x,
 // round trip on the dependent chain (~0.13 us a step); from LDS the loop is
 // compute-bound.  Otherwise the tsa 2 path of k_agc_chunks.
 constexpr long kAgcSmallMax = 8192;      // samples staged (64 KB of LDS)
-__global__ void __launch_bounds__(64) k_agc_small(const float2* __restrict__ x, long n, AgcState* st, int C, long nch,
+__device__ __forceinline__ void k_agc_small_body(const float2* __restrict__ x, long n, AgcState* st, int C, long nch,
                                                   float2* __restrict__ y, uint8_t* __restrict__ status, int perturb)
 {
     LDSP_LATENCY_CRITICAL();
@@ -403,6 +432,19 @@ __global__ void __launch_bounds__(64) k_agc_small(const float2* __restrict__ x, 
         if (reruns) st->pad[0] += reruns;     // ldsp_debug_agc_tsa_reruns
     }
 }
+struct AgcSmallArgs {
+    const float2* x;
+    long n;
+    AgcState* st;
+    int C;
+    long nch;
+    float2* y;
+    uint8_t* status;
+    int perturb;
+};
+__device__ __forceinline__ void k_agc_small_run(const AgcSmallArgs& a) { k_agc_small_body(a.x, a.n, a.st, a.C, a.nch, a.y, a.status, a.perturb); }
+LDSP_KERNEL_PAIR(k_agc_small, AgcSmallArgs, k_agc_small_run, 64)
+
 
 // Parallel repair round over runs of failed chunks.  flags (k_agc_flags)
 // mark the chunks whose guessed start state differs from the predecessor's
@@ -428,7 +470,7 @@ __device__ __forceinline__ bool agc_flag(const unsigned long long* flags, long c
     return (flags[c >> 6] >> (c & 63)) & 1ull;
 }
 
-__global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x, long n, const AgcState* st, int C,
+__device__ __forceinline__ void k_agc_runfix_body(const float2* __restrict__ x, long n, const AgcState* st, int C,
                                                    long nch, unsigned* __restrict__ sc,
                                                    const unsigned long long* __restrict__ flags,
                                                    float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg)
@@ -466,6 +508,21 @@ __global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x,
         gs[7] = r.timer;
     }
 }
+struct AgcRunfixArgs {
+    const float2* x;
+    long n;
+    const AgcState* st;
+    int C;
+    long nch;
+    unsigned* sc;
+    const unsigned long long* flags;
+    float2* y;
+    uint8_t* status;
+    unsigned* dbg;
+};
+__device__ __forceinline__ void k_agc_runfix_run(const AgcRunfixArgs& a) { k_agc_runfix_body(a.x, a.n, a.st, a.C, a.nch, a.sc, a.flags, a.y, a.status, a.dbg); }
+LDSP_KERNEL_PAIR(k_agc_runfix, AgcRunfixArgs, k_agc_runfix_run, 64)
+
 
 // Parallel pre-check: bit c of flags[c / 64] = chunk c's start state differs
 // from chunk c-1's end state (after the repair rounds).
@@ -473,7 +530,7 @@ __global__ void __launch_bounds__(64) k_agc_runfix(const float2* __restrict__ x,
 // state); 2 = the same, but chunk 0 is presumed right (repair rounds that run
 // before the previous call has produced the true state; k_agc_verify then
 // checks chunk 0 directly).
-__global__ void __launch_bounds__(64) k_agc_flags(int C, int W, long nch, const unsigned* __restrict__ sc,
+__device__ __forceinline__ void k_agc_flags_body(int C, int W, long nch, const unsigned* __restrict__ sc,
                                                   const AgcState* st, int spec, unsigned long long* __restrict__ flags)
 {
     LDSP_LATENCY_CRITICAL();
@@ -486,8 +543,20 @@ __global__ void __launch_bounds__(64) k_agc_flags(int C, int W, long nch, const 
     const unsigned long long m = __ballot(bad);
     if (threadIdx.x == 0) flags[blockIdx.x] = m;
 }
+struct AgcFlagsArgs {
+    int C;
+    int W;
+    long nch;
+    const unsigned* sc;
+    const AgcState* st;
+    int spec;
+    unsigned long long* flags;
+};
+__device__ __forceinline__ void k_agc_flags_run(const AgcFlagsArgs& a) { k_agc_flags_body(a.C, a.W, a.nch, a.sc, a.st, a.spec, a.flags); }
+LDSP_KERNEL_PAIR(k_agc_flags, AgcFlagsArgs, k_agc_flags_run, 64)
 
-__global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x, long n, AgcState* st, int C, int W,
+
+__device__ __forceinline__ void k_agc_verify_body(const float2* __restrict__ x, long n, AgcState* st, int C, int W,
                                                    int spec, long nch, unsigned* __restrict__ sc,
                                                    const unsigned long long* __restrict__ flags, float2* __restrict__ y,
                                                    uint8_t* __restrict__ status, unsigned* dbg)
@@ -553,6 +622,23 @@ __global__ void __launch_bounds__(64) k_agc_verify(const float2* __restrict__ x,
         st->timer = ldntu(e + 3);
     }
 }
+struct AgcVerifyArgs {
+    const float2* x;
+    long n;
+    AgcState* st;
+    int C;
+    int W;
+    int spec;
+    long nch;
+    unsigned* sc;
+    const unsigned long long* flags;
+    float2* y;
+    uint8_t* status;
+    unsigned* dbg;
+};
+__device__ __forceinline__ void k_agc_verify_run(const AgcVerifyArgs& a) { k_agc_verify_body(a.x, a.n, a.st, a.C, a.W, a.spec, a.nch, a.sc, a.flags, a.y, a.status, a.dbg); }
+LDSP_KERNEL_PAIR(k_agc_verify, AgcVerifyArgs, k_agc_verify_run, 64)
+
 
 __global__ void k_math_eval(int fn, const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y,
                             long n)
@@ -579,11 +665,8 @@ __global__ void k_math_eval(int fn, const float* __restrict__ a, const float* __
 void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
-    {
-        LDSP_PROF(s, "k_agc_seq");
-        hipLaunchKernelGGL(k_agc_seq, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, (float2*)y, status);
-    }
-    LDSP_HIP(hipGetLastError());
+    launch("k_agc_seq", k_agc_seq, k_agc_seq_many, dim3(1), dim3(64), 0, s,
+           AgcSeqArgs{(const float2*)x, (long)n, st, (float2*)y, status});
 }
 
 size_t agc_flags_offset_words(long nchunks) { return (size_t)nchunks * 8 + 8; }     // after records + debug words
@@ -593,19 +676,13 @@ void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, vo
 {
     if (n == 0) return;
     if ((p.tsa & 2) && p.nchunks <= 64 && (long)n <= kAgcSmallMax) {
-        LDSP_PROF(s, "k_agc_chunks");
-        hipLaunchKernelGGL(k_agc_small, dim3(1), dim3(64), n * sizeof(float2), s, (const float2*)x, (long)n, st, p.C,
-                           p.nchunks, (float2*)y, status, (p.tsa & 4) ? 1 : 0);
-        LDSP_HIP(hipGetLastError());
+        launch("k_agc_chunks", k_agc_small, k_agc_small_many, dim3(1), dim3(64), n * sizeof(float2), s,
+               AgcSmallArgs{(const float2*)x, (long)n, st, p.C, p.nchunks, (float2*)y, status, (p.tsa & 4) ? 1 : 0});
         return;
     }
-    {
-        LDSP_PROF(s, "k_agc_chunks");
-        hipLaunchKernelGGL(k_agc_chunks, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, (const float2*)x,
-                           (const float2*)p.hist, (long)p.H, (long)n, (const AgcState*)st, p.C, p.W, p.Wa, p.nchunks,
-                           (unsigned*)p.scratch, (float2*)y, status, p.tsa);
-    }
-    LDSP_HIP(hipGetLastError());
+    launch("k_agc_chunks", k_agc_chunks, k_agc_chunks_many, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s,
+           AgcChunksArgs{(const float2*)x, (const float2*)p.hist, (long)p.H, (long)n, (const AgcState*)st, p.C, p.W,
+                         p.Wa, p.nchunks, (unsigned*)p.scratch, (float2*)y, status, p.tsa});
 }
 
 static void agc_rounds(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, int spec,
@@ -614,20 +691,12 @@ static void agc_rounds(const void* x, size_t n, AgcState* st, const SpecPlan& p,
     unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
     const unsigned nb = (unsigned)((p.nchunks + 63) / 64);
     for (int round = 0; round <= p.rounds; round++) {
-        {
-            LDSP_PROF(s, "k_agc_flags");
-            hipLaunchKernelGGL(k_agc_flags, dim3(nb), dim3(64), 0, s, p.C, p.W, p.nchunks, (const unsigned*)p.scratch,
-                               (const AgcState*)st, spec, flags);
-        }
-        LDSP_HIP(hipGetLastError());
+        launch("k_agc_flags", k_agc_flags, k_agc_flags_many, dim3(nb), dim3(64), 0, s,
+               AgcFlagsArgs{p.C, p.W, p.nchunks, (const unsigned*)p.scratch, (const AgcState*)st, spec, flags});
         if (round == p.rounds) break;
-        {
-            LDSP_PROF(s, "k_agc_runfix");
-            hipLaunchKernelGGL(k_agc_runfix, dim3(nb), dim3(64), 0, s, (const float2*)x, (long)n,
-                               (const AgcState*)st, p.C, p.nchunks, (unsigned*)p.scratch,
-                               (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr);
-        }
-        LDSP_HIP(hipGetLastError());
+        launch("k_agc_runfix", k_agc_runfix, k_agc_runfix_many, dim3(nb), dim3(64), 0, s,
+               AgcRunfixArgs{(const float2*)x, (long)n, (const AgcState*)st, p.C, p.nchunks, (unsigned*)p.scratch,
+                             (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr});
     }
 }
 
@@ -635,13 +704,9 @@ static void agc_verify(const void* x, size_t n, AgcState* st, const SpecPlan& p,
                        hipStream_t s)
 {
     unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
-    {
-        LDSP_PROF(s, "k_agc_verify");
-        hipLaunchKernelGGL(k_agc_verify, dim3(1), dim3(64), 0, s, (const float2*)x, (long)n, st, p.C, p.W, spec,
-                           p.nchunks, (unsigned*)p.scratch, (const unsigned long long*)flags, (float2*)y, status,
-                           p.dbg ? p.dbg + p.rounds : nullptr);
-    }
-    LDSP_HIP(hipGetLastError());
+    launch("k_agc_verify", k_agc_verify, k_agc_verify_many, dim3(1), dim3(64), 0, s,
+           AgcVerifyArgs{(const float2*)x, (long)n, st, p.C, p.W, spec, p.nchunks, (unsigned*)p.scratch,
+                         (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + p.rounds : nullptr});
 }
 
 void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)

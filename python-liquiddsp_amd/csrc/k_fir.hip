@@ -18,6 +18,7 @@
 // NCO mix (nco_crcf_mix_block_{up,down}, reference src/nco.hpp:70,78):
 //   theta_i = theta_0 + i * dtheta (mod 2^32, exact), 1024-entry table in LDS.
 #include "resamp_dev.hpp"
+#include "batch.hpp"
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 
@@ -134,10 +135,10 @@ __global__ void __launch_bounds__(kThreads) k_fir_fast(const T* __restrict__ x, 
 constexpr int kExactOut = 256;
 
 template <typename T>
-__global__ void __launch_bounds__(kThreads) k_fir_exact(const T* __restrict__ x, const T* __restrict__ hist,
-                                                        T* __restrict__ hist_out, long n,
-                                                        const float* __restrict__ hrev, int L, float scale,
-                                                        T* __restrict__ y)
+__device__ __forceinline__ void k_fir_exact_body(const T* __restrict__ x, const T* __restrict__ hist,
+                                                 T* __restrict__ hist_out, long n,
+                                                 const float* __restrict__ hrev, int L, float scale,
+                                                 T* __restrict__ y)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* lds = reinterpret_cast<T*>(smem);
@@ -168,6 +169,29 @@ __global__ void __launch_bounds__(kThreads) k_fir_exact(const T* __restrict__ x,
     T r = z;
     for (int i = 0; i < L; i++) r = vmac(r, hrev[i], lds[tid + i]);
     y[o] = vscale(r, scale);
+}
+
+template <typename T>
+struct FirExactArgs {
+    const T* x;
+    const T* hist;
+    T* hist_out;
+    long n;
+    const float* hrev;
+    int L;
+    float scale;
+    T* y;
+};
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_fir_exact(FirExactArgs<T> a)
+{
+    k_fir_exact_body<T>(a.x, a.hist, a.hist_out, a.n, a.hrev, a.L, a.scale, a.y);
+}
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_fir_exact_many(Many<FirExactArgs<T>> m)
+{
+    const FirExactArgs<T>& a = m.a[blockIdx.y];
+    k_fir_exact_body<T>(a.x, a.hist, a.hist_out, a.n, a.hrev, a.L, a.scale, a.y);
 }
 
 template <typename T>
@@ -211,13 +235,12 @@ void fir_exact_t(const void* x, const void* hist, void* hist_out, size_t n, cons
     if (lds > 64 * 1024)
         LDSP_HIP(hipFuncSetAttribute((const void*)k_fir_exact<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
+    if (lds > 64 * 1024)
+        LDSP_HIP(hipFuncSetAttribute((const void*)k_fir_exact_many<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
     const unsigned grid = (unsigned)((n + kExactOut - 1) / kExactOut);
-    {
-        LDSP_PROF(s, "k_fir_exact");
-        hipLaunchKernelGGL(k_fir_exact<T>, dim3(grid), dim3(kThreads), lds, s, (const T*)x, (const T*)hist,
-                           (T*)hist_out, (long)n, taps, L, scale, (T*)y);
-    }
-    LDSP_HIP(hipGetLastError());
+    launch("k_fir_exact", k_fir_exact<T>, k_fir_exact_many<T>, dim3(grid), dim3(kThreads), lds, s,
+           FirExactArgs<T>{(const T*)x, (const T*)hist, (T*)hist_out, (long)n, taps, L, scale, (T*)y});
 }
 
 template <typename T>

@@ -18,6 +18,7 @@
 //             and re-runs the (rare) chunks that did not coalesce.
 #include <type_traits>
 
+#include "batch.hpp"
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 #include "ldsp_math.hpp"
@@ -195,9 +196,9 @@ __device__ __forceinline__ void run_f32(StepF&& step, const float* __restrict__ 
 // read LDS.  From global memory each batch of 8 steps waited an L2 / HBM round
 // trip (~150 ns a step for a first-order filter, whose step is ~10 ns).
 template <int Z, bool STAGE>
-__global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* __restrict__ xg, long n, int ncomp,
-                                                        const float* __restrict__ state0, int C, int W, long nch,
-                                                        float* __restrict__ sc, float* __restrict__ y)
+__device__ __forceinline__ void k_iir_spec_chunks_body(const IirDesc& d, const float* __restrict__ xg, long n, int ncomp,
+                                                       const float* __restrict__ state0, int C, int W, long nch,
+                                                       float* __restrict__ sc, float* __restrict__ y)
 {
     LDSP_LATENCY_CRITICAL();
     extern __shared__ float xs[];
@@ -257,15 +258,38 @@ __global__ void __launch_bounds__(64) k_iir_spec_chunks(IirDesc d, const float* 
             if (i < d.nv) endst[i] = v[i];
     }
 }
+struct IirSpecChunksArgs {
+    IirDesc d;
+    const float* xg;
+    long n;
+    int ncomp;
+    const float* state0;
+    int C, W;
+    long nch;
+    float* sc;
+    float* y;
+};
+template <int Z, bool STAGE>
+__global__ void __launch_bounds__(64) k_iir_spec_chunks(IirSpecChunksArgs a)
+{
+    k_iir_spec_chunks_body<Z, STAGE>(a.d, a.xg, a.n, a.ncomp, a.state0, a.C, a.W, a.nch, a.sc, a.y);
+}
+template <int Z, bool STAGE>
+__global__ void __launch_bounds__(64) k_iir_spec_chunks_many(Many<IirSpecChunksArgs> m)
+{
+    const IirSpecChunksArgs& a = m.a[blockIdx.y];
+    k_iir_spec_chunks_body<Z, STAGE>(a.d, a.xg, a.n, a.ncomp, a.state0, a.C, a.W, a.nch, a.sc, a.y);
+}
+
 
 // Verifier: one wave walks the chunks in order.  Chunk k's outputs are exact
 // iff its guessed start state equals chunk k-1's (exact) end state bit for bit
 // (chunks whose warm-up reached the call start began from the true state).
 // Parallel pre-check: bit c of flags[c / 64] = chunk c's guessed start state
 // differs from chunk c-1's end state (before any re-run).
-__global__ void __launch_bounds__(64) k_iir_spec_flags(IirDesc d, int ncomp, int C, int W, long nch,
-                                                       const float* __restrict__ sc,
-                                                       unsigned long long* __restrict__ flags)
+__device__ __forceinline__ void k_iir_spec_flags_body(const IirDesc& d, int ncomp, int C, int W, long nch,
+                                                      const float* __restrict__ sc,
+                                                      unsigned long long* __restrict__ flags)
 {
     LDSP_LATENCY_CRITICAL();
     const int fs = fstate_size(d);
@@ -280,14 +304,27 @@ __global__ void __launch_bounds__(64) k_iir_spec_flags(IirDesc d, int ncomp, int
     const unsigned long long m = __ballot(bad);
     if (threadIdx.x == 0) flags[blockIdx.x] = m;
 }
+struct IirSpecFlagsArgs {
+    IirDesc d;
+    int ncomp, C, W;
+    long nch;
+    const float* sc;
+    unsigned long long* flags;
+};
+__device__ __forceinline__ void k_iir_spec_flags_run(const IirSpecFlagsArgs& a)
+{
+    k_iir_spec_flags_body(a.d, a.ncomp, a.C, a.W, a.nch, a.sc, a.flags);
+}
+LDSP_KERNEL_PAIR(k_iir_spec_flags, IirSpecFlagsArgs, k_iir_spec_flags_run, 64)
+
 
 __device__ __forceinline__ uint32_t rl_u32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
 
 template <int Z>
-__global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* __restrict__ x, long n, int ncomp,
-                                                        int C, int W, long nch, float* __restrict__ sc,
-                                                        const unsigned long long* __restrict__ flags,
-                                                        float* __restrict__ state, float* __restrict__ y)
+__device__ __forceinline__ void k_iir_spec_verify_body(const IirDesc& d, const float* __restrict__ x, long n, int ncomp,
+                                                       int C, int W, long nch, float* __restrict__ sc,
+                                                       const unsigned long long* __restrict__ flags,
+                                                       float* __restrict__ state, float* __restrict__ y)
 {
     LDSP_LATENCY_CRITICAL();
     const int lane = threadIdx.x;
@@ -369,6 +406,29 @@ __global__ void __launch_bounds__(64) k_iir_spec_verify(IirDesc d, const float* 
     // carried state = end state of the last chunk
     for (int i = lane; i < per; i += 64) state[i] = ldnt(sc + ((nch - 1) * 2 + 1) * per + i);
 }
+struct IirSpecVerifyArgs {
+    IirDesc d;
+    const float* x;
+    long n;
+    int ncomp, C, W;
+    long nch;
+    float* sc;
+    const unsigned long long* flags;
+    float* state;
+    float* y;
+};
+template <int Z>
+__global__ void __launch_bounds__(64) k_iir_spec_verify(IirSpecVerifyArgs a)
+{
+    k_iir_spec_verify_body<Z>(a.d, a.x, a.n, a.ncomp, a.C, a.W, a.nch, a.sc, a.flags, a.state, a.y);
+}
+template <int Z>
+__global__ void __launch_bounds__(64) k_iir_spec_verify_many(Many<IirSpecVerifyArgs> m)
+{
+    const IirSpecVerifyArgs& a = m.a[blockIdx.y];
+    k_iir_spec_verify_body<Z>(a.d, a.x, a.n, a.ncomp, a.C, a.W, a.nch, a.sc, a.flags, a.state, a.y);
+}
+
 
 // --------------------------------------------------------------- float64 scan
 // double state vector per component: SOS [2s, 2s+1] = (v0, v1) of section s
@@ -962,45 +1022,38 @@ void iir_spec(bool cplx, const IirDesc& d, const void* x, size_t n, float* state
     const long work = p.nchunks * ncomp;
     const int z = iir_size_class(d);
     {
-        LDSP_PROF(s, "k_iir_spec_chunks");
         // a workgroup's window: 64 / ncomp chunks of C samples + W, ncomp floats each
         const size_t stage = (size_t)4 * (64 * (size_t)p.C + (size_t)ncomp * p.W);
         const bool st = stage <= 64 * 1024;
-        auto launch = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned)((work + 63) / 64)), dim3(64), st ? stage : 0, s, d,
-                               (const float*)x, (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks,
-                               (float*)p.scratch, (float*)y);
-        };
+        const IirSpecChunksArgs a{d, (const float*)x, (long)n, ncomp, (const float*)state, p.C, p.W, p.nchunks,
+                                  (float*)p.scratch, (float*)y};
+        const dim3 g((unsigned)((work + 63) / 64)), b(64);
+        const size_t shm = st ? stage : 0;
+#define SPEC_CHUNKS(Z, S) launch("k_iir_spec_chunks", k_iir_spec_chunks<Z, S>, k_iir_spec_chunks_many<Z, S>, g, b, shm, s, a)
         if (st) {
-            if (z == 2) launch(k_iir_spec_chunks<2, true>);
-            else if (z == 4) launch(k_iir_spec_chunks<4, true>);
-            else launch(k_iir_spec_chunks<kMaxTf, true>);
+            if (z == 2) SPEC_CHUNKS(2, true);
+            else if (z == 4) SPEC_CHUNKS(4, true);
+            else SPEC_CHUNKS(kMaxTf, true);
         } else {
-            if (z == 2) launch(k_iir_spec_chunks<2, false>);
-            else if (z == 4) launch(k_iir_spec_chunks<4, false>);
-            else launch(k_iir_spec_chunks<kMaxTf, false>);
+            if (z == 2) SPEC_CHUNKS(2, false);
+            else if (z == 4) SPEC_CHUNKS(4, false);
+            else SPEC_CHUNKS(kMaxTf, false);
         }
+#undef SPEC_CHUNKS
     }
-    LDSP_HIP(hipGetLastError());
     const int fs = d.sos ? 3 * d.nsos : d.nv;
     unsigned long long* flags = (unsigned long long*)((char*)p.scratch + spec_flags_offset(p.nchunks, ncomp, fs));
+    launch("k_iir_spec_flags", k_iir_spec_flags, k_iir_spec_flags_many, dim3((unsigned)((p.nchunks + 63) / 64)),
+           dim3(64), 0, s, IirSpecFlagsArgs{d, ncomp, p.C, p.W, p.nchunks, (const float*)p.scratch, flags});
     {
-        LDSP_PROF(s, "k_iir_spec_flags");
-        hipLaunchKernelGGL(k_iir_spec_flags, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s, d, ncomp, p.C,
-                           p.W, p.nchunks, (const float*)p.scratch, flags);
+        const IirSpecVerifyArgs a{d, (const float*)x, (long)n, ncomp, p.C, p.W, p.nchunks, (float*)p.scratch,
+                                  (const unsigned long long*)flags, state, (float*)y};
+#define SPEC_VERIFY(Z) launch("k_iir_spec_verify", k_iir_spec_verify<Z>, k_iir_spec_verify_many<Z>, dim3(1), dim3(64), 0, s, a)
+        if (z == 2) SPEC_VERIFY(2);
+        else if (z == 4) SPEC_VERIFY(4);
+        else SPEC_VERIFY(kMaxTf);
+#undef SPEC_VERIFY
     }
-    LDSP_HIP(hipGetLastError());
-    {
-        LDSP_PROF(s, "k_iir_spec_verify");
-        auto launch = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, s, d, (const float*)x, (long)n, ncomp, p.C, p.W, p.nchunks,
-                               (float*)p.scratch, (const unsigned long long*)flags, state, (float*)y);
-        };
-        if (z == 2) launch(k_iir_spec_verify<2>);
-        else if (z == 4) launch(k_iir_spec_verify<4>);
-        else launch(k_iir_spec_verify<kMaxTf>);
-    }
-    LDSP_HIP(hipGetLastError());
 }
 
 void iir_scan(bool cplx, const IirDesc& d, const void* x, size_t n, double* state64, const IirScanPlan& p, void* y,

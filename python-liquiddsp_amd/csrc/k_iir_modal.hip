@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "batch.hpp"
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 #include "ldsp_math.hpp"
@@ -276,10 +277,10 @@ __device__ __forceinline__ void add_mat(const double* __restrict__ P, const Moda
 #define LDSP_MODAL_WPE 1
 #endif
 template <int NC, int M, bool IQ16, bool RS = false>
-__global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalCoef cf, const void* __restrict__ xv, long n, long nw,
-                                                       IirModalPlan p, const double* __restrict__ st_in,
-                                                       double* __restrict__ st_out, float* __restrict__ yv,
-                                                       IirResampFuse f)
+__device__ __forceinline__ void k_iir_modal_body(const IirModalCoef& cf, const void* __restrict__ xv, long n, long nw,
+                                                 const IirModalPlan& p, const double* __restrict__ st_in,
+                                                 double* __restrict__ st_out, float* __restrict__ yv,
+                                                 const IirResampFuse& f)
 {
     constexpr int kGran = M * 4;        // {half, epoch} granules per published component state
     __shared__ float pl[NC][64 * kRow];
@@ -493,6 +494,28 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
     else tile_store<NC, false>(ry, tid, pl);
 }
 
+struct IirModalArgs {
+    IirModalCoef cf;
+    const void* xv;
+    long n, nw;
+    IirModalPlan p;
+    const double* st_in;
+    double* st_out;
+    float* yv;
+    IirResampFuse f;
+};
+template <int NC, int M, bool IQ16, bool RS = false>
+__global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalArgs a)
+{
+    k_iir_modal_body<NC, M, IQ16, RS>(a.cf, a.xv, a.n, a.nw, a.p, a.st_in, a.st_out, a.yv, a.f);
+}
+template <int NC, int M, bool IQ16, bool RS = false>
+__global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal_many(Many<IirModalArgs> m)
+{
+    const IirModalArgs& a = m.a[blockIdx.y];
+    k_iir_modal_body<NC, M, IQ16, RS>(a.cf, a.xv, a.n, a.nw, a.p, a.st_in, a.st_out, a.yv, a.f);
+}
+
 // IIR -> resampler fusion, the outputs whose window straddles a unit boundary:
 // one thread per unit u, for the outputs whose window ends in u's first H samples
 // (their earlier samples: unit u - 1's tail, or the resampler history before the
@@ -503,8 +526,8 @@ __global__ void __launch_bounds__(64 * NC, LDSP_MODAL_WPE) k_iir_modal(IirModalC
 // Block 0 also writes the resampler's new history (the call's last H filter
 // outputs).  Same arithmetic and order as the resampler kernels.
 template <int NC>
-__global__ void __launch_bounds__(256) k_iir_resamp_edges(IirResampFuse f, long n, long nw,
-                                                          const float* __restrict__ hist, float* __restrict__ hist_out)
+__device__ __forceinline__ void k_iir_resamp_edges_body(const IirResampFuse& f, long n, long nw,
+                                                        const float* __restrict__ hist, float* __restrict__ hist_out)
 {
     const int H = f.sub_len - 1;
     auto sample = [&](long g, int c) -> float {
@@ -584,14 +607,39 @@ __global__ void __launch_bounds__(256) k_iir_resamp_edges(IirResampFuse f, long 
     }
 }
 
+struct IirResampEdgesArgs {
+    IirResampFuse f;
+    long n, nw;
+    const float* hist;
+    float* hist_out;
+};
+template <int NC>
+__global__ void __launch_bounds__(256) k_iir_resamp_edges(IirResampEdgesArgs a)
+{
+    k_iir_resamp_edges_body<NC>(a.f, a.n, a.nw, a.hist, a.hist_out);
+}
+template <int NC>
+__global__ void __launch_bounds__(256) k_iir_resamp_edges_many(Many<IirResampEdgesArgs> m)
+{
+    const IirResampEdgesArgs& a = m.a[blockIdx.y];
+    k_iir_resamp_edges_body<NC>(a.f, a.n, a.nw, a.hist, a.hist_out);
+}
+
 template <int NC, int M, bool IQ16, bool RS = false>
 void launch_modal(const IirModalCoef& cf, const void* x, size_t n, const double* st_in, double* st_out,
                   const IirModalPlan& p, float* y, hipStream_t s, const IirResampFuse& f = IirResampFuse{})
 {
     const long nw = iir_modal_units(n);
-    LDSP_PROF(s, RS ? "k_iir_modal_rs" : "k_iir_modal");
-    hipLaunchKernelGGL((k_iir_modal<NC, M, IQ16, RS>), dim3((unsigned)(p.one_xcd ? 8 * nw : nw)), dim3(64 * NC), 0, s,
-                       cf, x, (long)n, nw, p, st_in, st_out, y, f);
+    // blocks b = q mod 8 share an XCD (the kernel's unit ranges): a merged launch
+    // keeps that only when every object's grid is a multiple of 8 (batch.hpp)
+    const IirModalArgs a{cf, x, (long)n, nw, p, st_in, st_out, y, f};
+    const dim3 g((unsigned)(p.one_xcd ? 8 * nw : nw)), b(64 * NC);
+    if constexpr (IQ16)
+        launch<IirModalArgs>(RS ? "k_iir_modal_rs" : "k_iir_modal", k_iir_modal<NC, M, IQ16, RS>, nullptr, g, b, 0, s, a,
+                             true);
+    else
+        launch<IirModalArgs>(RS ? "k_iir_modal_rs" : "k_iir_modal", k_iir_modal<NC, M, IQ16, RS>,
+                             k_iir_modal_many<NC, M, IQ16, RS>, g, b, 0, s, a, true);
 }
 
 } // namespace
@@ -621,17 +669,13 @@ void iir_modal_resamp(bool cplx, const IirModalCoef& cf, const void* x, size_t n
     default: throw Error(LDSP_EUNSUP, "iir: unsupported number of modes");
     }
 #undef LDSP_MODAL
-    LDSP_HIP(hipGetLastError());
     const long nw = iir_modal_units(n);
-    LDSP_PROF(s, "k_iir_resamp_edges");
     const unsigned g = (unsigned)((nw + 255) / 256);
+    const IirResampEdgesArgs a{f, (long)n, nw, (const float*)hist, (float*)hist_out};
     if (cplx)
-        hipLaunchKernelGGL(k_iir_resamp_edges<2>, dim3(g), dim3(256), 0, s, f, (long)n, nw, (const float*)hist,
-                           (float*)hist_out);
+        launch("k_iir_resamp_edges", k_iir_resamp_edges<2>, k_iir_resamp_edges_many<2>, dim3(g), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(k_iir_resamp_edges<1>, dim3(g), dim3(256), 0, s, f, (long)n, nw, (const float*)hist,
-                           (float*)hist_out);
-    LDSP_HIP(hipGetLastError());
+        launch("k_iir_resamp_edges", k_iir_resamp_edges<1>, k_iir_resamp_edges_many<1>, dim3(g), dim3(256), 0, s, a);
 }
 
 void iir_modal(bool cplx, const IirModalCoef& cf, const void* x, size_t n, const double* st_in, double* st_out,

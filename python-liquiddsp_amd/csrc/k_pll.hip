@@ -30,6 +30,7 @@
 #include <atomic>
 #include <cstdlib>
 
+#include "batch.hpp"
 #include "kernels.hpp"
 #include "ldsp_common.hpp"
 #include "ldsp_math.hpp"
@@ -86,7 +87,7 @@ __device__ __forceinline__ Kick pll_eval(const float* tab, uint32_t i, float2 u0
 constexpr int kSeqChunk = 2048;
 
 template <bool COSTAS>
-__global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st, int gcur, float* __restrict__ y)
+__device__ __forceinline__ void k_pll_seq_body(PllIn in, long n, AmpState* st, int gcur, float* __restrict__ y)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
@@ -119,6 +120,23 @@ __global__ void __launch_bounds__(256) k_pll_seq(PllIn in, long n, AmpState* st,
         st->gd[1 - gcur] = d;
     }
 }
+struct PllSeqArgs {
+    PllIn in;
+    long n;
+    AmpState* st;
+    int gcur;
+    float* y;
+};
+
+template <bool COSTAS>
+__global__ void __launch_bounds__(256) k_pll_seq(PllSeqArgs a) { k_pll_seq_body<COSTAS>(a.in, a.n, a.st, a.gcur, a.y); }
+template <bool COSTAS>
+__global__ void __launch_bounds__(256) k_pll_seq_many(::ldsp::Many<PllSeqArgs> m)
+{
+    const PllSeqArgs& a = m.a[blockIdx.y];
+    k_pll_seq_body<COSTAS>(a.in, a.n, a.st, a.gcur, a.y);
+}
+
 
 // Carrier-mode sequential loop with candidate kicks (the technique of
 // k_fm_pll, k_misc.hip): a step's kicks and output are a function of the
@@ -159,7 +177,7 @@ __device__ __forceinline__ SqCand sq_cands(const float2* b0, const float2* b1, i
     return c;
 }
 
-__global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st, int gcur, float* __restrict__ y)
+__device__ __forceinline__ void k_pll_seqc_body(PllIn in, long n, AmpState* st, int gcur, float* __restrict__ y)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
@@ -243,6 +261,17 @@ __global__ void __launch_bounds__(256) k_pll_seqc(PllIn in, long n, AmpState* st
         st->gd[1 - gcur] = d;
     }
 }
+
+struct PllSeqcArgs {
+    PllIn in;
+    long n;
+    AmpState* st;
+    int gcur;
+    float* y;
+};
+__device__ __forceinline__ void k_pll_seqc_run(const PllSeqcArgs& a) { k_pll_seqc_body(a.in, a.n, a.st, a.gcur, a.y); }
+LDSP_KERNEL_PAIR(k_pll_seqc, PllSeqcArgs, k_pll_seqc_run, 256)
+
 
 // ------------------------------------------------------------------ candidates
 // Candidate chunks of kCand samples.  Per sample the candidate kernel writes
@@ -430,7 +459,7 @@ __device__ __forceinline__ void cand_warm_approx(const PllIn& in, long a, long b
 // previous call's walker; the walker carries the exact offset either way.
 // from_true: start from the true state instead of the guess (Costas, whose
 // front waits for the previous walk: chunk 0 is then the true trajectory's branch).
-__global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st, int gcur, CandBuf cb,
+__device__ __forceinline__ void k_pll_cand_body(PllIn in, long n, AmpState* st, int gcur, CandBuf cb,
                                                  float* __restrict__ y, int warm, int from_true, int approx)
 {
     LDSP_LATENCY_CRITICAL();
@@ -465,9 +494,24 @@ __global__ void __launch_bounds__(64) k_pll_cand(PllIn in, long n, AmpState* st,
     }
 }
 
+struct PllCandArgs {
+    PllIn in;
+    long n;
+    AmpState* st;
+    int gcur;
+    CandBuf cb;
+    float* y;
+    int warm;
+    int from_true;
+    int approx;
+};
+__device__ __forceinline__ void k_pll_cand_run(const PllCandArgs& a) { k_pll_cand_body(a.in, a.n, a.st, a.gcur, a.cb, a.y, a.warm, a.from_true, a.approx); }
+LDSP_KERNEL_PAIR(k_pll_cand, PllCandArgs, k_pll_cand_run, 64)
+
+
 // Costas: re-run the chunks the first scan marked (hk) from their start state
 // turned by half a turn, so every candidate sits in chunk 0's branch.
-__global__ void __launch_bounds__(64) k_pll_reflip(PllIn in, long n, AmpState* st, CandBuf cb, float* __restrict__ y)
+__device__ __forceinline__ void k_pll_reflip_body(PllIn in, long n, AmpState* st, CandBuf cb, float* __restrict__ y)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
@@ -484,6 +528,17 @@ __global__ void __launch_bounds__(64) k_pll_reflip(PllIn in, long n, AmpState* s
     cb.ce[2 * k + 1] = d;
     cb.cnt[k] = nent;
 }
+
+struct PllReflipArgs {
+    PllIn in;
+    long n;
+    AmpState* st;
+    CandBuf cb;
+    float* y;
+};
+__device__ __forceinline__ void k_pll_reflip_run(const PllReflipArgs& a) { k_pll_reflip_body(a.in, a.n, a.st, a.cb, a.y); }
+LDSP_KERNEL_PAIR(k_pll_reflip, PllReflipArgs, k_pll_reflip_run, 64)
+
 
 // ------------------------------------------------------------------ walker offset model
 // The true trajectory T and chunk k's candidate C_k (samples [b_k, b_k + 256))
@@ -523,7 +578,7 @@ __device__ __forceinline__ uint32_t half_flip(uint32_t dth, int flip)
     return flip ? ((dth + (1u << 30)) >> 31) : 0u;
 }
 
-__global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
+__device__ __forceinline__ void k_pll_scan_body(CandBuf cb, int flip)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ uint32_t sa[1024], sb[1024], sc[1024], sh[1024];
@@ -579,6 +634,14 @@ __global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
     if (t == 1023) *cb.ne = sa[1023];
 }
 
+struct PllScanArgs {
+    CandBuf cb;
+    int flip;
+};
+__device__ __forceinline__ void k_pll_scan_run(const PllScanArgs& a) { k_pll_scan_body(a.cb, a.flip); }
+LDSP_KERNEL_PAIR(k_pll_scan, PllScanArgs, k_pll_scan_run, 1024)
+
+
 // Entry records, one wave per chunk (4 samples per lane).  Per entry (SoA per
 // walker block: E0[kBlkE], E1[kBlkE]), with srel = s - S_blk (< 2^17):
 //   E0 = (c, W, srel, L' - dk2)
@@ -590,7 +653,7 @@ __global__ void __launch_bounds__(1024) k_pll_scan(CandBuf cb, int flip)
 //        x_post - L' <= span (see below), i.e. x_pre - (L' - dk2) <= span with the
 //        offset before the repair (x_post = x_pre + dk2), which the walker keeps.
 // The tail of the last walker block is padded with W = ~0 (never an event).
-__global__ void __launch_bounds__(256) k_pll_entries(PllIn in, const AmpState* st, CandBuf cb, long n)
+__device__ __forceinline__ void k_pll_entries_body(PllIn in, const AmpState* st, CandBuf cb, long n)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
@@ -670,6 +733,16 @@ __global__ void __launch_bounds__(256) k_pll_entries(PllIn in, const AmpState* s
             cb.ent[(size_t)(t / kBlkE) * 2 * kBlkE + t % kBlkE] = make_uint4(0u, ~0u, 0u, 0u);
     }
 }
+
+struct PllEntriesArgs {
+    PllIn in;
+    const AmpState* st;
+    CandBuf cb;
+    long n;
+};
+__device__ __forceinline__ void k_pll_entries_run(const PllEntriesArgs& a) { k_pll_entries_body(a.in, a.st, a.cb, a.n); }
+LDSP_KERNEL_PAIR(k_pll_entries, PllEntriesArgs, k_pll_entries_run, 256)
+
 
 // ------------------------------------------------------------------ walker
 struct WalkBufE {
@@ -1404,7 +1477,7 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
 // Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + kRing - 1
 // into the LDS ring meanwhile.
 template <bool F24, bool STATS, int VAR = 0>
-__global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, AmpState* st, CandBuf cb,
+__device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, CandBuf cb,
                                                            float* __restrict__ y)
 {
     LDSP_LATENCY_CRITICAL();
@@ -1634,8 +1707,25 @@ __global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllIn in, long n, Amp
         }
     }
 }
+struct PllWalkArgs {
+    PllIn in;
+    long n;
+    AmpState* st;
+    CandBuf cb;
+    float* y;
+};
 
-__global__ void k_delay_hist(const float2* __restrict__ x, const float2* __restrict__ hist, float2* __restrict__ hist_out,
+template <bool F24, bool STATS, int VAR = 0>
+__global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllWalkArgs a) { k_pll_walk_body<F24, STATS, VAR>(a.in, a.n, a.st, a.cb, a.y); }
+template <bool F24, bool STATS, int VAR = 0>
+__global__ void __launch_bounds__(kWalkThreads) k_pll_walk_many(::ldsp::Many<PllWalkArgs> m)
+{
+    const PllWalkArgs& a = m.a[blockIdx.y];
+    k_pll_walk_body<F24, STATS, VAR>(a.in, a.n, a.st, a.cb, a.y);
+}
+
+
+__device__ __forceinline__ void k_delay_hist_body(const float2* __restrict__ x, const float2* __restrict__ hist, float2* __restrict__ hist_out,
                              long n, int m)
 {
     LDSP_LATENCY_CRITICAL();
@@ -1644,6 +1734,16 @@ __global__ void k_delay_hist(const float2* __restrict__ x, const float2* __restr
         hist_out[j] = g >= 0 ? x[g] : hist[g + m];
     }
 }
+struct DelayHistArgs {
+    const float2* x;
+    const float2* hist;
+    float2* hist_out;
+    long n;
+    int m;
+};
+__device__ __forceinline__ void k_delay_hist_run(const DelayHistArgs& a) { k_delay_hist_body(a.x, a.hist, a.hist_out, a.n, a.m); }
+LDSP_KERNEL_PAIR(k_delay_hist, DelayHistArgs, k_delay_hist_run, 256)
+
 
 } // namespace
 
@@ -1684,11 +1784,8 @@ size_t pll_stats_offset(size_t n) { return pll_layout(n).stats; }
 void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m, hipStream_t s)
 {
     if (m <= 0) return;
-    {
-        LDSP_PROF(s, "k_delay_hist");
-        hipLaunchKernelGGL(k_delay_hist, dim3(1), dim3(256), 0, s, (const float2*)x, (const float2*)hist,
-                           (float2*)hist_out, (long)n, m);
-    }
+    launch("k_delay_hist", k_delay_hist, k_delay_hist_many, dim3(1), dim3(256), 0, s,
+           DelayHistArgs{(const float2*)x, (const float2*)hist, (float2*)hist_out, (long)n, m});
     LDSP_HIP(hipGetLastError());
 }
 
@@ -1760,95 +1857,71 @@ void pll_front(const PllCall& c, hipStream_t s)
 {
     if (c.n == 0) return;
     // delay-line history for the next call (m samples); this call's kernels read the old one
-    {
-        LDSP_PROF(s, "k_delay_hist");
-        hipLaunchKernelGGL(k_delay_hist, dim3(1), dim3(64), 0, s, (const float2*)c.x, (const float2*)c.hist,
-                           (float2*)c.hist_out, (long)c.n, c.m);
-    }
-    LDSP_HIP(hipGetLastError());
+    launch("k_delay_hist", k_delay_hist, k_delay_hist_many, dim3(1), dim3(64), 0, s,
+           DelayHistArgs{(const float2*)c.x, (const float2*)c.hist, (float2*)c.hist_out, (long)c.n, c.m});
     if (!pll_parallel(c.n, c.costas)) return;
     const CandBuf cb = cand_buf(c);
     {
-        LDSP_PROF(s, "k_pll_cand");
         static const int warm = LDSP_KNOB("LDSP_PLL_WARM", kWarm);
         // carrier loop: approximate warm-up (cand_warm_approx); Costas keeps the exact one
         // (its two stable points make the warm-up's branch matter, k_pll_reflip)
         static const int approx = LDSP_KNOB("LDSP_PLL_WARM_APPROX", 1);
-        hipLaunchKernelGGL(k_pll_cand, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s, pll_in(c), (long)c.n,
-                           c.st, c.gcur, cb, c.y, warm, c.costas, (approx && !c.costas) ? 1 : 0);
+        launch("k_pll_cand", k_pll_cand, k_pll_cand_many, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s,
+               PllCandArgs{pll_in(c), (long)c.n, c.st, c.gcur, cb, c.y, warm, c.costas,
+                           (approx && !c.costas) ? 1 : 0});
     }
-    LDSP_HIP(hipGetLastError());
     if (c.costas) {
-        {
-            LDSP_PROF(s, "k_pll_scan");
-            hipLaunchKernelGGL(k_pll_scan, dim3(1), dim3(1024), 0, s, cb, 1);
-        }
-        LDSP_HIP(hipGetLastError());
-        {
-            LDSP_PROF(s, "k_pll_reflip");
-            hipLaunchKernelGGL(k_pll_reflip, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s, pll_in(c),
-                               (long)c.n, c.st, cb, c.y);
-        }
-        LDSP_HIP(hipGetLastError());
+        launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(1024), 0, s, PllScanArgs{cb, 1});
+        launch("k_pll_reflip", k_pll_reflip, k_pll_reflip_many, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s,
+               PllReflipArgs{pll_in(c), (long)c.n, c.st, cb, c.y});
     }
-    {
-        LDSP_PROF(s, "k_pll_scan");
-        hipLaunchKernelGGL(k_pll_scan, dim3(1), dim3(1024), 0, s, cb, 0);
-    }
-    LDSP_HIP(hipGetLastError());
-    {
-        LDSP_PROF(s, "k_pll_entries");
-        hipLaunchKernelGGL(k_pll_entries, dim3((unsigned)((cb.nchc + 3) / 4)), dim3(256), 0, s, pll_in(c),
-                           (const AmpState*)c.st, cb, (long)c.n);
-    }
-    LDSP_HIP(hipGetLastError());
+    launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(1024), 0, s, PllScanArgs{cb, 0});
+    launch("k_pll_entries", k_pll_entries, k_pll_entries_many, dim3((unsigned)((cb.nchc + 3) / 4)), dim3(256), 0, s,
+           PllEntriesArgs{pll_in(c), (const AmpState*)c.st, cb, (long)c.n});
 }
 
 void pll_back(const PllCall& c, hipStream_t s)
 {
     if (c.n == 0) return;
     if (!pll_parallel(c.n, c.costas)) {
-        if (c.costas) {
-            LDSP_PROF(s, "k_pll_seq");
-            hipLaunchKernelGGL(k_pll_seq<true>, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
-        } else {
-            LDSP_PROF(s, "k_pll_seqc");
-            hipLaunchKernelGGL(k_pll_seqc, dim3(1), dim3(256), 0, s, pll_in(c), (long)c.n, c.st, c.gcur, c.y);
-        }
-        LDSP_HIP(hipGetLastError());
+        if (c.costas)
+            launch("k_pll_seq", k_pll_seq<true>, k_pll_seq_many<true>, dim3(1), dim3(256), 0, s,
+                   PllSeqArgs{pll_in(c), (long)c.n, c.st, c.gcur, c.y});
+        else
+            launch("k_pll_seqc", k_pll_seqc, k_pll_seqc_many, dim3(1), dim3(256), 0, s,
+                   PllSeqcArgs{pll_in(c), (long)c.n, c.st, c.gcur, c.y});
         return;
     }
     {
-        LDSP_PROF(s, "k_pll_walk");
         static const bool stats = LDSP_KNOB("LDSP_DEBUG_PLL", 0) != 0;
         // the walker stores repaired outputs through 32-bit byte offsets from y
         LDSP_REQUIRE(c.n < (size_t(1) << 30), "ampmodem: at most 2^30 samples per call");
         const dim3 g(1), blk(kWalkThreads);
-        const PllIn in = pll_in(c);
-        const CandBuf cb = cand_buf(c);
+        const PllWalkArgs a{pll_in(c), (long)c.n, c.st, cand_buf(c), c.y};
+#define WALK_LAUNCH(F, S, V) launch("k_pll_walk", k_pll_walk<F, S, V>, k_pll_walk_many<F, S, V>, g, blk, 0, s, a)
         if (c.alpha_host <= 1.0f / 512.0f) {
 #ifdef LDSP_TUNING
             // timing variants (k_pll_walk VAR): read per call
             const int var = LDSP_KNOB("LDSP_WALK_VARIANT", 0);
             if (!stats && var > 0) {
-#define WALK_VAR(V) case V: hipLaunchKernelGGL((k_pll_walk<true, false, V>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y); break;
                 switch (var) {
-                WALK_VAR(32) WALK_VAR(64) WALK_VAR(96) WALK_VAR(128)
+                case 32: WALK_LAUNCH(true, false, 32); break;
+                case 64: WALK_LAUNCH(true, false, 64); break;
+                case 96: WALK_LAUNCH(true, false, 96); break;
+                case 128: WALK_LAUNCH(true, false, 128); break;
                 default: break;
                 }
-#undef WALK_VAR
-                LDSP_HIP(hipGetLastError());
                 return;
             }
 #endif
-            if (stats) hipLaunchKernelGGL((k_pll_walk<true, true>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y);
-            else hipLaunchKernelGGL((k_pll_walk<true, false>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y);
+            if (stats) WALK_LAUNCH(true, true, 0);
+            else WALK_LAUNCH(true, false, 0);
         } else {
-            if (stats) hipLaunchKernelGGL((k_pll_walk<false, true>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y);
-            else hipLaunchKernelGGL((k_pll_walk<false, false>), g, blk, 0, s, in, (long)c.n, c.st, cb, c.y);
+            if (stats) WALK_LAUNCH(false, true, 0);
+            else WALK_LAUNCH(false, false, 0);
         }
+#undef WALK_LAUNCH
     }
-    LDSP_HIP(hipGetLastError());
 }
 
 } // namespace k

@@ -115,6 +115,13 @@ struct DeviceGuard {
     }
 };
 
+// Many-calls (batch.hpp): while a recorder is active on this thread, stream
+// waits and event records are recorded in call order instead of issued.
+class BatchRecorder;
+BatchRecorder* batch_active();
+void batch_record_wait(hipEvent_t ev);
+void batch_record_mark(hipEvent_t ev);
+
 // Cross-stream order of one object's device state.  An execute marks the point
 // on its stream where the object's state (and the scratch it reuses) is final;
 // an execute enqueued on a different stream first waits for that point, so
@@ -132,11 +139,14 @@ struct StreamMark {
         if (ev) (void)hipEventDestroy(ev);
     }
     void wait(hipStream_t t) const {
-        if (set && s != t) LDSP_HIP(hipStreamWaitEvent(t, ev, 0));
+        if (!(set && s != t)) return;
+        if (batch_active()) batch_record_wait(ev);
+        else LDSP_HIP(hipStreamWaitEvent(t, ev, 0));
     }
     void mark(hipStream_t t) {
         if (!ev) LDSP_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        LDSP_HIP(hipEventRecord(ev, t));
+        if (batch_active()) batch_record_mark(ev);
+        else LDSP_HIP(hipEventRecord(ev, t));
         s = t;
         set = true;
     }

@@ -1177,6 +1177,116 @@ PYBIND11_MODULE(_liquiddsp, m)
         "resampler(iir(x)) in one pass (the filter's outputs stay on chip when it takes the fast modal scan): "
         "same output bits and state updates as the two calls");
 
+    // ---- many-calls: one call on each of C objects of one class, one launch per kernel
+    // for all of them (ldsp_*_many; device tensors on the current device's stream)
+    m.def(
+        "execute_many",
+        [](py::list objs, py::list xs) {
+            const size_t C = py::len(objs);
+            if (C == 0) return py::list();
+            if (py::len(xs) != C) throw py::value_error("execute_many: one input per object");
+            std::vector<DevIn> ins;
+            for (size_t c = 0; c < C; c++) {
+                if (!is_device_tensor(xs[c])) throw py::value_error("execute_many: device tensors only");
+                ins.push_back(dev_in(xs[c], true));
+                if (ins[c].n != ins[0].n) throw py::value_error("execute_many: every input must have the same length");
+            }
+            const size_t n = ins[0].n;
+            py::object o0 = objs[0];
+            std::vector<const void*> xp;
+            for (auto& d : ins) xp.push_back(d.ptr);
+            py::list outs;
+            std::vector<void*> yp;
+            auto mk = [&](bool cout) {
+                for (size_t c = 0; c < C; c++) {
+                    py::object t = dev_empty(n, cout, ins[c].device);
+                    yp.push_back(tptr(t));
+                    outs.append(t);
+                }
+            };
+            if (py::isinstance<AGC>(o0)) {
+                std::vector<ldsp_agc_t> q;
+                for (size_t c = 0; c < C; c++) {
+                    AGC& a = objs[c].cast<AGC&>();
+                    if (a.mSquelch) throw py::value_error("execute_many: AGC with squelch on (onRise replay) not supported");
+                    q.push_back(a.q);
+                }
+                mk(true);
+                check(ldsp_agc_execute_many(q.data(), xp.data(), n, yp.data(), (int)C, ins[0].stream));
+                for (size_t c = 0; c < C; c++) g_state_last = 7;
+            } else if (py::isinstance<AmpModem>(o0)) {
+                std::vector<ldsp_ampmodem_t> q;
+                for (size_t c = 0; c < C; c++) q.push_back(objs[c].cast<AmpModem&>().q);
+                mk(false);
+                check(ldsp_ampmodem_demodulate_many(q.data(), xp.data(), n, yp.data(), (int)C, ins[0].stream));
+            } else {
+                std::vector<ldsp_iirfilt_t> q;
+                bool cplx = as_iir(o0).cplx;
+                for (size_t c = 0; c < C; c++) {
+                    IIR& f = as_iir(objs[c]);
+                    if (f.cplx != cplx) throw py::value_error("execute_many: mixed real and complex filters");
+                    q.push_back(f.q);
+                }
+                if (!cplx) {                      // real filters take float32 inputs
+                    ins.clear();
+                    xp.clear();
+                    for (size_t c = 0; c < C; c++) {
+                        ins.push_back(dev_in(xs[c], false));
+                        xp.push_back(ins[c].ptr);
+                    }
+                }
+                mk(cplx);
+                check(ldsp_iirfilt_execute_many(q.data(), xp.data(), n, yp.data(), (int)C, ins[0].stream));
+            }
+            return outs;
+        },
+        py::arg("objects"), py::arg("inputs"),
+        "[obj(x) for obj, x in zip(objects, inputs)] with one kernel launch per stage for all objects: AGC, "
+        "AmpModem or IIR filter objects of one class, device tensors of equal length; same bits as the separate calls");
+    m.def(
+        "filter_resample_many",
+        [](py::list iirs, py::list rss, py::list xs) {
+            const size_t C = py::len(iirs);
+            if (C == 0) return py::list();
+            if (py::len(rss) != C || py::len(xs) != C) throw py::value_error("filter_resample_many: one resampler and input per filter");
+            std::vector<ldsp_iirfilt_t> q;
+            std::vector<ldsp_resamp_t> r;
+            std::vector<DevIn> ins;
+            std::vector<const void*> xp;
+            bool c0 = as_resampler(rss[0]).cplx;
+            for (size_t c = 0; c < C; c++) {
+                IIR& f = as_iir(iirs[c]);
+                Resampler& rs = as_resampler(rss[c]);
+                if (f.cplx != c0 || rs.cplx != c0) throw py::value_error("filter_resample_many: mixed real and complex");
+                q.push_back(f.q);
+                r.push_back(rs.q);
+                if (!is_device_tensor(xs[c])) throw py::value_error("filter_resample_many: device tensors only");
+                ins.push_back(dev_in(xs[c], c0));
+                if (ins[c].n != ins[0].n) throw py::value_error("filter_resample_many: every input must have the same length");
+                xp.push_back(ins[c].ptr);
+            }
+            const size_t n = ins[0].n;
+            size_t cap = 0;
+            std::vector<size_t> k(C);
+            for (size_t c = 0; c < C; c++) {
+                check(ldsp_resamp_num_outputs(r[c], n, &k[c]));
+                cap = std::max(cap, k[c]);
+            }
+            py::list outs;
+            std::vector<void*> yp;
+            for (size_t c = 0; c < C; c++) {
+                py::object t = dev_empty(k[c], c0, ins[c].device);
+                yp.push_back(tptr(t));
+                outs.append(t);
+            }
+            std::vector<size_t> nout(C);
+            check(ldsp_iirfilt_resamp_execute_many(q.data(), r.data(), xp.data(), n, yp.data(), cap, nout.data(),
+                                                   (int)C, ins[0].stream));
+            return outs;
+        },
+        py::arg("iirs"), py::arg("resamplers"), py::arg("inputs"),
+        "[filter_resample(f, r, x) for f, r, x in zip(...)] with one kernel launch per stage for all channels");
+
     // ---- bytes_to_iq, Delay (wrapper.cpp:13, 25-28)
     m.def("bytes_to_iq", &bytes_to_iq, py::arg("byts"));
     py::class_<Delay>(m, "Delay")
