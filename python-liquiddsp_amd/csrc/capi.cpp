@@ -2213,7 +2213,7 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
             const int c64 = (int)(((n + 63) / 64 + 31) / 32 * 32);      // 64 chunks of a multiple of 32
             p.C = tsa ? (c64 <= 256 ? std::max(tsa_cmin, c64) : 256) : agc_c;
             p.nchunks = (long)((n + p.C - 1) / p.C);
-            p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks), q->device);
+            p.scratch = q->scr[sl].ensure(k::agc_scratch_bytes(p.nchunks, p.C), q->device);
             p.hist = q->hist[h3].p;
             p.H = spec ? (int)hl : 0;
             // a small call's chunks in one wave check and repair themselves (tsa 2:

@@ -195,6 +195,73 @@ __device__ __forceinline__ void agc_run(AgcReg& r, const AgcState& p, const X& x
     else agc_run_t<OUT, true>(r, p, x, a, b, y, status);
 }
 
+// A chunk's exact run with its state checkpointed every kAgcCp samples
+// (STORE: the chunk kernel records its speculative trajectory) or compared
+// with those checkpoints (!STORE: a re-run from the true state stops at the
+// first checkpoint its state equals bit for bit -- from there the stored
+// outputs and end state are the true ones, so a re-run costs the trajectories'
+// coalescence time, ~110 samples on the bench chain, instead of the chunk;
+// every checkpoint it passes without a match is rewritten, so the checkpoints
+// always describe the trajectory the stored outputs hold).
+// cpk: the chunk's kAgcCp-spaced states, [j][4 words] for offsets kAgcCp (j + 1)
+// < chunk length.  Returns true when a re-run coalesced (r then holds the state
+// at that checkpoint; the caller takes the stored end state).
+constexpr int kAgcCp = 64;
+static_assert(kAgcCp % kB == 0, "checkpoints fall on batch ends");
+__device__ __forceinline__ bool cp_equal(const AgcReg& r, const unsigned* c)
+{
+    return c[0] == __float_as_uint(r.g) && c[1] == __float_as_uint(r.y2p) && c[2] == (unsigned)r.mode &&
+           c[3] == r.timer;
+}
+template <bool STORE, bool SQ>
+__device__ __forceinline__ bool agc_run_cp_t(AgcReg& r, const AgcState& p, const float2* __restrict__ x, long a, long b,
+                                             float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* cpk)
+{
+    if (a >= b) return false;
+    const long full = a + (b - a) / kB * kB;
+    float2 nx[kB];
+#pragma unroll
+    for (int j = 0; j < kB; j++) nx[j] = x[min(a + j, b - 1)];
+    long i = a;
+    for (; i < full; i += kB) {
+        float2 cx[kB];
+#pragma unroll
+        for (int j = 0; j < kB; j++) cx[j] = nx[j];
+#pragma unroll
+        for (int j = 0; j < kB; j++) nx[j] = x[min(i + kB + j, b - 1)];
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            const float2 v = agc_step<SQ>(r, p, cx[j]);
+            y[i + j] = v;
+            if (status) status[i + j] = (uint8_t)r.mode;
+        }
+        const long o = i + kB - a;                     // samples done
+        if (o % kAgcCp == 0 && i + kB < b) {
+            unsigned* c = cpk + (o / kAgcCp - 1) * 4;
+            if (!STORE && cp_equal(r, c)) return true;
+            // the outputs up to here are this run's now: so is the checkpoint (a later
+            // re-run of this chunk must compare against the trajectory the outputs hold)
+            c[0] = __float_as_uint(r.g);
+            c[1] = __float_as_uint(r.y2p);
+            c[2] = (unsigned)r.mode;
+            c[3] = r.timer;
+        }
+    }
+    for (; i < b; i++) {
+        const float2 v = agc_step<SQ>(r, p, x[i]);
+        y[i] = v;
+        if (status) status[i] = (uint8_t)r.mode;
+    }
+    return false;
+}
+template <bool STORE>
+__device__ __forceinline__ bool agc_run_cp(AgcReg& r, const AgcState& p, const float2* __restrict__ x, long a, long b,
+                                           float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* cpk)
+{
+    if (p.mode == SQ_DISABLED) return agc_run_cp_t<STORE, false>(r, p, x, a, b, y, status, cpk);
+    return agc_run_cp_t<STORE, true>(r, p, x, a, b, y, status, cpk);
+}
+
 // One lane runs the loop; the wave stages the input through LDS 2048 samples
 // at a time so the loop never waits on a global load.
 __device__ __forceinline__ void k_agc_seq_body(const float2* __restrict__ x, long n, AgcState* st,
@@ -246,7 +313,7 @@ constexpr int kPow = kAgcPow;
 __device__ __forceinline__ void k_agc_chunks_body(const float2* __restrict__ x, const float2* __restrict__ hist, long H,
                                                    long n, const AgcState* st, int C, int W, int Wa, long nch,
                                                    unsigned* __restrict__ sc, float2* __restrict__ y,
-                                                   uint8_t* __restrict__ status, int tsa)
+                                                   uint8_t* __restrict__ status, int tsa, unsigned* cp)
 {
     LDSP_LATENCY_CRITICAL();
     const long chunk = (long)blockIdx.x * 64 + threadIdx.x;
@@ -354,7 +421,8 @@ __device__ __forceinline__ void k_agc_chunks_body(const float2* __restrict__ x, 
     gs[1] = __float_as_uint(r.y2p);
     gs[2] = (unsigned)r.mode;
     gs[3] = r.timer;
-    agc_run<true>(r, p, x, s0, s1, y, status);
+    if (cp) agc_run_cp<true>(r, p, x, s0, s1, y, status, cp + chunk * (C / kAgcCp) * 4);
+    else agc_run<true>(r, p, x, s0, s1, y, status);
     gs[4] = __float_as_uint(r.g);
     gs[5] = __float_as_uint(r.y2p);
     gs[6] = (unsigned)r.mode;
@@ -374,8 +442,9 @@ struct AgcChunksArgs {
     float2* y;
     uint8_t* status;
     int tsa;
+    unsigned* cp;
 };
-__device__ __forceinline__ void k_agc_chunks_run(const AgcChunksArgs& a) { k_agc_chunks_body(a.x, a.hist, a.H, a.n, a.st, a.C, a.W, a.Wa, a.nch, a.sc, a.y, a.status, a.tsa); }
+__device__ __forceinline__ void k_agc_chunks_run(const AgcChunksArgs& a) { k_agc_chunks_body(a.x, a.hist, a.H, a.n, a.st, a.C, a.W, a.Wa, a.nch, a.sc, a.y, a.status, a.tsa, a.cp); }
 LDSP_KERNEL_PAIR(k_agc_chunks, AgcChunksArgs, k_agc_chunks_run, 64)
 
 
@@ -473,7 +542,8 @@ __device__ __forceinline__ bool agc_flag(const unsigned long long* flags, long c
 __device__ __forceinline__ void k_agc_runfix_body(const float2* __restrict__ x, long n, const AgcState* st, int C,
                                                    long nch, unsigned* __restrict__ sc,
                                                    const unsigned long long* __restrict__ flags,
-                                                   float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg)
+                                                   float2* __restrict__ y, uint8_t* __restrict__ status, unsigned* dbg,
+                                                   unsigned* cp)
 {
     LDSP_LATENCY_CRITICAL();
     const long k = (long)blockIdx.x * 64 + threadIdx.x;
@@ -501,7 +571,12 @@ __device__ __forceinline__ void k_agc_runfix_body(const float2* __restrict__ x, 
         gs[2] = (unsigned)r.mode;
         gs[3] = r.timer;
         const long s0 = m * C;
-        agc_run<true>(r, p, x, s0, min(n, s0 + C), y, status);
+        if (cp && agc_run_cp<false>(r, p, x, s0, min(n, s0 + C), y, status, cp + m * (C / kAgcCp) * 4)) {
+            // coalesced with the stored trajectory: its outputs and end state stand
+            r = AgcReg{__uint_as_float(ldntu(gs + 4)), __uint_as_float(ldntu(gs + 5)), (int)ldntu(gs + 6), ldntu(gs + 7)};
+            continue;
+        }
+        if (!cp) agc_run<true>(r, p, x, s0, min(n, s0 + C), y, status);
         gs[4] = __float_as_uint(r.g);
         gs[5] = __float_as_uint(r.y2p);
         gs[6] = (unsigned)r.mode;
@@ -519,8 +594,9 @@ struct AgcRunfixArgs {
     float2* y;
     uint8_t* status;
     unsigned* dbg;
+    unsigned* cp;
 };
-__device__ __forceinline__ void k_agc_runfix_run(const AgcRunfixArgs& a) { k_agc_runfix_body(a.x, a.n, a.st, a.C, a.nch, a.sc, a.flags, a.y, a.status, a.dbg); }
+__device__ __forceinline__ void k_agc_runfix_run(const AgcRunfixArgs& a) { k_agc_runfix_body(a.x, a.n, a.st, a.C, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
 LDSP_KERNEL_PAIR(k_agc_runfix, AgcRunfixArgs, k_agc_runfix_run, 64)
 
 
@@ -559,7 +635,7 @@ LDSP_KERNEL_PAIR(k_agc_flags, AgcFlagsArgs, k_agc_flags_run, 64)
 __device__ __forceinline__ void k_agc_verify_body(const float2* __restrict__ x, long n, AgcState* st, int C, int W,
                                                    int spec, long nch, unsigned* __restrict__ sc,
                                                    const unsigned long long* __restrict__ flags, float2* __restrict__ y,
-                                                   uint8_t* __restrict__ status, unsigned* dbg)
+                                                   uint8_t* __restrict__ status, unsigned* dbg, unsigned* cp)
 {
     LDSP_LATENCY_CRITICAL();
     const int lane = threadIdx.x;
@@ -600,10 +676,14 @@ __device__ __forceinline__ void k_agc_verify_body(const float2* __restrict__ x, 
         if (lane == 0) {
             AgcReg r{__uint_as_float(pred_word(sc, st, kb, 0)), __uint_as_float(pred_word(sc, st, kb, 1)),
                      (int)pred_word(sc, st, kb, 2), pred_word(sc, st, kb, 3)};
-            agc_run<true>(r, p, x, kb * C, min(n, kb * C + C), y, status);
+            unsigned* en = sc + kb * 8;
+            if (cp && agc_run_cp<false>(r, p, x, kb * C, min(n, kb * C + C), y, status, cp + kb * (C / kAgcCp) * 4))
+                r = AgcReg{__uint_as_float(ldntu(en + 4)), __uint_as_float(ldntu(en + 5)), (int)ldntu(en + 6),
+                           ldntu(en + 7)};      // coalesced: the stored end state stands
+            else if (!cp)
+                agc_run<true>(r, p, x, kb * C, min(n, kb * C + C), y, status);
             if (dbg) dbg[0]++;
             st->pad[1]++;                                   // ldsp_debug_agc_reruns (verifier)
-            unsigned* en = sc + kb * 8;
             en[4] = __float_as_uint(r.g);
             en[5] = __float_as_uint(r.y2p);
             en[6] = (unsigned)r.mode;
@@ -635,8 +715,9 @@ struct AgcVerifyArgs {
     float2* y;
     uint8_t* status;
     unsigned* dbg;
+    unsigned* cp;
 };
-__device__ __forceinline__ void k_agc_verify_run(const AgcVerifyArgs& a) { k_agc_verify_body(a.x, a.n, a.st, a.C, a.W, a.spec, a.nch, a.sc, a.flags, a.y, a.status, a.dbg); }
+__device__ __forceinline__ void k_agc_verify_run(const AgcVerifyArgs& a) { k_agc_verify_body(a.x, a.n, a.st, a.C, a.W, a.spec, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
 LDSP_KERNEL_PAIR(k_agc_verify, AgcVerifyArgs, k_agc_verify_run, 64)
 
 
@@ -670,7 +751,18 @@ void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hi
 }
 
 size_t agc_flags_offset_words(long nchunks) { return (size_t)nchunks * 8 + 8; }     // after records + debug words
-size_t agc_scratch_bytes(long nchunks) { return (agc_flags_offset_words(nchunks) + 2 * ((nchunks + 63) / 64 + 64)) * 4; }
+// then the flag words, then the checkpoints: [nchunks][C / kAgcCp][4 words] (chunk-parallel calls)
+static size_t agc_cp_offset_words(long nchunks) { return agc_flags_offset_words(nchunks) + 2 * ((nchunks + 63) / 64 + 64); }
+size_t agc_scratch_bytes(long nchunks, int C)
+{
+    return (agc_cp_offset_words(nchunks) + (size_t)nchunks * (size_t)(C / kAgcCp) * 4) * 4;
+}
+// checkpoints for chunks of C >= 2 kAgcCp samples outside the small-call paths
+static unsigned* agc_cp(const SpecPlan& p)
+{
+    return (!(p.tsa & 3) && p.C >= 2 * kAgcCp && p.C % kAgcCp == 0) ? (unsigned*)p.scratch + agc_cp_offset_words(p.nchunks)
+                                                                      : nullptr;
+}
 
 void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
 {
@@ -682,7 +774,7 @@ void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, vo
     }
     launch("k_agc_chunks", k_agc_chunks, k_agc_chunks_many, dim3((unsigned)((p.nchunks + 63) / 64)), dim3(64), 0, s,
            AgcChunksArgs{(const float2*)x, (const float2*)p.hist, (long)p.H, (long)n, (const AgcState*)st, p.C, p.W,
-                         p.Wa, p.nchunks, (unsigned*)p.scratch, (float2*)y, status, p.tsa});
+                         p.Wa, p.nchunks, (unsigned*)p.scratch, (float2*)y, status, p.tsa, agc_cp(p)});
 }
 
 static void agc_rounds(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, int spec,
@@ -696,7 +788,8 @@ static void agc_rounds(const void* x, size_t n, AgcState* st, const SpecPlan& p,
         if (round == p.rounds) break;
         launch("k_agc_runfix", k_agc_runfix, k_agc_runfix_many, dim3(nb), dim3(64), 0, s,
                AgcRunfixArgs{(const float2*)x, (long)n, (const AgcState*)st, p.C, p.nchunks, (unsigned*)p.scratch,
-                             (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr});
+                             (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr,
+                             agc_cp(p)});
     }
 }
 
@@ -706,7 +799,8 @@ static void agc_verify(const void* x, size_t n, AgcState* st, const SpecPlan& p,
     unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
     launch("k_agc_verify", k_agc_verify, k_agc_verify_many, dim3(1), dim3(64), 0, s,
            AgcVerifyArgs{(const float2*)x, (long)n, st, p.C, p.W, spec, p.nchunks, (unsigned*)p.scratch,
-                         (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + p.rounds : nullptr});
+                         (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + p.rounds : nullptr,
+                         agc_cp(p)});
 }
 
 void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)

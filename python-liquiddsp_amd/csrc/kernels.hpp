@@ -203,7 +203,7 @@ struct AgcState {         // device-resident agc_crcf state
 };
 constexpr int kAgcPow = 256;     // samples whose mean power sets a chunk's guessed gain
 void agc_seq(const void* x, size_t n, AgcState* st, void* y, uint8_t* status, hipStream_t s);
-size_t agc_scratch_bytes(long nchunks);
+size_t agc_scratch_bytes(long nchunks, int C);
 // Chunk-parallel exact AGC in two halves.  Front: the chunks (reads only the
 // parameters when p.H > 0, so it may run while the previous call's back half
 // still advances the state).  Back: flag / repair rounds and the verifier

@@ -234,3 +234,30 @@ def test_filter_resample_other_rates(ld, rng, rate, fc):
             ref = rb(fb(xd[a:b]))
             assert y.shape == ref.shape
             assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), (cplx, a, b)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_filter_resample_vs_oracle_1Mi(ld, ora, exact):
+    """filter_resample against the restatement directly (not only against the two
+    GPU calls), on a 1 Mi prefix of the bench channel: exact mode (the two-call
+    fallback) bit for bit against the float32 restatement (IIR -> resampler);
+    fast mode (the fused modal scan) against the restatement's float64 IIR
+    followed by its resampler, within the SURVEY 8(d) 1e-6 bound (two float64
+    evaluations of one filter, each rounded once to float32)."""
+    import torch
+    import bench
+    n = 1 << 20
+    xd = bench.synth_channel(n, 0, torch.device("cuda", 0))
+    x = xd.cpu().numpy()
+    f = ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2000000)
+    r = ld.ComplexResampler(rate=48000 / 2000000, Fc=48000 / 2000000)
+    f.exact = exact
+    y = torch.cat([ld.filter_resample(f, r, xd[:300_000]), ld.filter_resample(f, r, xd[300_000:])]).cpu().numpy()
+    oi = ora.IIRFilter(prototype=("cheby2", "lowpass", 1, 8, np.float32(15000 / 2000000), 0.3, 0.7, 60.0))
+    orr = ora.Resampler(np.float32(48000 / 2000000), m=20, fc=np.float32(48000 / 2000000), npfb=13, cplx=True)
+    ref = orr(oi(x) if exact else oi.execute_f64(x))
+    assert y.shape == ref.shape and y.size > 25_000
+    if exact:
+        assert np.array_equal(bits(y), bits(ref))
+    else:
+        assert maxrel(y, ref) <= 1e-6, maxrel(y, ref)
