@@ -2911,15 +2911,27 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
 // recorded work is issued with the launches of objects that run the same
 // kernel on the same grid merged (blockIdx.y = object).  Device memory only;
 // the objects must be distinct.
+// `batchable(c)`: object c's call takes a path whose every kernel has a merged
+// form; otherwise the objects run one after another (the same bits, C times the
+// launches) -- e.g. exact-mode IIR filters, single-sideband AmpModems.
 extern "C++" {
-template <class T, class F>
-static int run_many(T* const* q, int C, void* stream, F&& one)
+template <class T, class B, class F>
+static int run_many(T* const* q, int C, void* stream, B&& batchable, F&& one)
 {
     return guard([&] {
         LDSP_REQUIRE(q != nullptr && C >= 1 && C <= 4096, "many: 1 .. 4096 objects");
         for (int c = 0; c < C; c++) {
             LDSP_REQUIRE(q[c] != nullptr, "many: NULL object");
             for (int c2 = 0; c2 < c; c2++) LDSP_REQUIRE(q[c2] != q[c], "many: the objects must be distinct");
+        }
+        bool all = true;
+        for (int c = 0; c < C; c++) all = all && batchable(c);
+        if (!all) {
+            for (int c = 0; c < C; c++) {
+                const int rc = one(c);
+                if (rc != LDSP_OK) throw Error(rc, g_last_error);
+            }
+            return;
         }
         BatchRecorder rec(C, (hipStream_t)stream);
         int rc = LDSP_OK;
@@ -2938,7 +2950,7 @@ static int run_many(T* const* q, int C, void* stream, F&& one)
 int ldsp_agc_execute_many(ldsp_agc_t* q, const void* const* x, size_t n, void* const* y, int C, void* stream)
 {
     LDSP_RANGE("ldsp_agc_execute_many");
-    return run_many(q, C, stream, [&](int c) {
+    return run_many(q, C, stream, [](int) { return true; }, [&](int c) {
         return ldsp_agc_execute(q[c], x[c], n, y[c], nullptr, LDSP_MEM_DEVICE, stream);
     });
 }
@@ -2947,7 +2959,7 @@ int ldsp_ampmodem_demodulate_many(ldsp_ampmodem_t* q, const void* const* x, size
                                   void* stream)
 {
     LDSP_RANGE("ldsp_ampmodem_demodulate_many");
-    return run_many(q, C, stream, [&](int c) {
+    return run_many(q, C, stream, [&](int c) { return q[c]->type == 0; }, [&](int c) {
         return ldsp_ampmodem_demodulate(q[c], x[c], n, y[c], LDSP_MEM_DEVICE, stream);
     });
 }
@@ -2956,6 +2968,9 @@ int ldsp_iirfilt_execute_many(ldsp_iirfilt_t* q, const void* const* x, size_t n,
 {
     LDSP_RANGE("ldsp_iirfilt_execute_many");
     return run_many(q, C, stream, [&](int c) {
+        const IirObj::Path p = q[c]->path_for(n);
+        return p == IirObj::kSpec || p == IirObj::kModal;
+    }, [&](int c) {
         return ldsp_iirfilt_execute(q[c], x[c], n, y[c], LDSP_MEM_DEVICE, stream);
     });
 }
@@ -2970,7 +2985,10 @@ int ldsp_iirfilt_resamp_execute_many(ldsp_iirfilt_t* q, ldsp_resamp_t* rs, const
                 set_last_error("many: the objects must be distinct");
                 return LDSP_EINVAL;
             }
-    return run_many(q, C, stream, [&](int c) {
+    return run_many(q, C, stream, [&](int c) {       // the fused pass (ldsp_iirfilt_resamp_execute)
+        return rs && rs[c] && q[c]->cplx == rs[c]->cplx && q[c]->path_for(n) == IirObj::kModal &&
+               rs[c]->sub_len >= 2 && rs[c]->sub_len - 1 <= 1024u;
+    }, [&](int c) {
         return ldsp_iirfilt_resamp_execute(q[c], rs[c], x[c], n, y[c], cap, nout ? nout + c : nullptr,
                                            LDSP_MEM_DEVICE, stream);
     });

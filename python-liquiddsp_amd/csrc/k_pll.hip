@@ -1793,10 +1793,14 @@ void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m
 // from kParMin (1 280) samples: their latency is the warm-up plus one recorded chunk
 // (~0.94 ms), then the walk.
 static const size_t kParMin = (size_t)LDSP_KNOB("LDSP_PLL_PARMIN", 1280L);
-// Carrier mode: the candidate-kick sequential loop (k_pll_seqc, ~0.29 us per
-// sample) beats candidates + walk up to ~2 k samples per call (the README's
-// 65 536-sample block gives 1 573: 451 us against 643 us of candidates alone).
-static const size_t kParMinCarrier = (size_t)LDSP_KNOB("LDSP_PLL_PARMIN_CARRIER", 2048L);
+// Carrier mode: the candidate-kick sequential loop (k_pll_seqc, ~0.25 us per
+// sample) against candidates + walk.  With exact candidate warm-ups the
+// candidates alone took 643 us for a README block (65 536 IQ -> 1 573 PCM
+// samples) and the threshold was 2 048; with the approximate warm-up
+// (cand_warm_approx) the parallel path wins from ~1 k samples: README blocks on
+// one stream 0.69 -> 0.54 ms (95 -> 120 MS/s), numpy blocks 0.89 -> 0.74 ms
+// (profiles/r05h_readme_blocks_*.json).
+static const size_t kParMinCarrier = (size_t)LDSP_KNOB("LDSP_PLL_PARMIN_CARRIER", 1024L);
 bool pll_parallel(size_t n, int costas) { return n >= (costas ? kParMin : kParMinCarrier); }
 
 static PllIn pll_in(const PllCall& c)

@@ -127,3 +127,23 @@ def test_many_rejects_bad_input(ld):
         ld.execute_many([g, ld.AGC()], [x, x[:5000]])        # unequal lengths
     with pytest.raises(ValueError):
         ld.execute_many([g], [x.cpu().numpy()])              # host arrays
+
+
+def test_many_unbatchable_paths_fall_back(ld):
+    # exact-mode IIR filters and single-sideband AmpModems take paths without merged
+    # kernels: the many-call runs the objects one after another, same bits
+    import torch
+    C, n = 3, 200_000
+    xs = [torch.from_numpy(_synth(n, c)).cuda() for c in range(C)]
+    fa = [ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2e6) for _ in range(C)]
+    fb = [ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2e6) for _ in range(C)]
+    for f in fa + fb:
+        f.exact = True
+    got = ld.execute_many(fa, xs)
+    for c in range(C):
+        assert torch.equal(got[c].view(torch.int64), fb[c](xs[c]).view(torch.int64)), c
+    ma = [ld.AmpModem(modulation=0.5, type="usb", carrier=True) for _ in range(C)]
+    mb = [ld.AmpModem(modulation=0.5, type="usb", carrier=True) for _ in range(C)]
+    got = ld.execute_many(ma, [x[:20_000] * 5 for x in xs])
+    for c in range(C):
+        assert torch.equal(got[c].view(torch.int32), mb[c](xs[c][:20_000] * 5).view(torch.int32)), c
