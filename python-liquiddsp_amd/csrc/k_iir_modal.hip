@@ -247,17 +247,16 @@ __device__ __forceinline__ void modal_run(const IirModalCoef& cf, Modal<M>& z, f
     for (int s = 0; s < kC; s++) {
         const bool on = !GUARD || s < cnt;
         const double ud = (double)row[s];
-        double y0 = cf.d * ud, y1 = 0.0;
+        double y = cf.d * ud;
 #pragma unroll
         for (int k = 0; k < M; k++) {
-            double& y = (k & 1) ? y1 : y0;
             y = fma(cf.c1[k], z.w0[k], y);
             y = fma(cf.c2[k], z.w1[k], y);
             const double w = fma(-cf.a1[k], z.w0[k], fma(-cf.a2[k], z.w1[k], ud));
             z.w1[k] = on ? z.w0[k] : z.w1[k];
             z.w0[k] = on ? w : z.w0[k];
         }
-        row[s] = (float)(y0 + y1);
+        row[s] = (float)y;
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -319,6 +318,9 @@ __device__ __forceinline__ void k_iir_modal_body(const IirModalCoef& cf, const v
         else tile_load<NC, IQ16, false>(rx, tid, pl);
     }
     __syncthreads();
+    // the unit's publication (pass 1, scan, BL_w) is what later units wait for:
+    // issue it ahead of other waves' pass 2 on this SIMD
+    __builtin_amdgcn_s_setprio(2);
     float* row = pl[c] + lane * kRow;  // this lane's chunk of its component: input, then output
     float u[kC];                        // pass 1 only; pass 2 reads the plane again
 #pragma unroll
@@ -346,6 +348,7 @@ __device__ __forceinline__ void k_iir_modal_body(const IirModalCoef& cf, const v
         }
     }
 
+    __builtin_amdgcn_s_setprio(0);
     // look-back: lane i < jw fetches BL_{w-1-i} (S_call when i == w)
 #ifdef LDSP_TUNING
     const int jw = (p.variant & 1) ? 0 : (int)min((long)p.J, w + 1);

@@ -13,6 +13,11 @@
 #   chains      scripts/chains_bench.py
 #   channels    scripts/channels_run.py (8 AMRadio chains on one GPU)
 #   c3spread    config-3 launch spread study (scripts/c3_spread.py)
+#   iirpmc      scripts/iir_pmc.sh (k_iir_modal kernel stats, HBM bytes, SQ / VALU-type counters)
+#   c3ab        config 3 (firbench) with build_ab/ (the previous build) and the product, twice, alternating
+#   ab:<file>:<pkg>,<pkg>..  a script with each package build in turn (LDSP_PKG_DIR), twice
+#   sqab:<pkg>,..  SQ issue counters of k_iir_modal per package build (scripts/iir_sq_ab.sh)
+#   ubench:<b>  a prebuilt microbenchmark scripts/ubench/<b>
 #   prof        rocprofv3 kernel stats + PMC passes (scripts/prof_round.sh TAG)
 #   py:<file>   python <file> (a one-off script under scripts/)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -47,6 +52,17 @@ for step in "$@"; do
     channels) run channels 400 python -u scripts/channels_run.py ;;
     c3spread) FIRBENCH_REPS=16 PMC_OUT="$o/c3" run c3pmc 600 bash scripts/fir_c3_pmc.sh
               python scripts/c3_spread.py "$o/c3" > "$o/c3_spread.json"; head -c 1500 "$o/c3_spread.json"; echo ;;
+    iirpmc) IIRPMC_OUT="$o/iirpmc" run iirpmc 900 bash scripts/iir_pmc.sh
+            python scripts/pmc_kernel.py "$o/iirpmc" > "$o/iirpmc_summary.json"; head -c 2500 "$o/iirpmc_summary.json"; echo ;;
+    c3ab) for pk in build_ab python-liquiddsp_amd build_ab python-liquiddsp_amd; do
+            FIRBENCH_N=1048576 FIRBENCH_TAPS=255 FIRBENCH_REPS=12 LDSP_PKG_DIR=$pk run "c3_$(basename $pk)" 300 python -u scripts/firbench.py
+          done ;;
+    ab:*) spec=${step#ab:}; f=${spec%%:*}; pkgs=${spec#*:}
+          for rep in 1 2; do for pk in $(echo "$pkgs" | tr ',' ' '); do
+            LDSP_PKG_DIR=$pk run "ab_$(basename "$f" .py)_$(basename "$pk")_$rep" 300 python -u "$f"
+          done; done ;;
+    sqab:*) pk=${step#sqab:}; run sqab 600 bash scripts/iir_sq_ab.sh "$o/sqab" $(echo "$pk" | tr ',' ' '); cat "$o/sqab.log" | grep -v '^$' | tail -8 ;;
+    ubench:*) f=${step#ubench:}; run "ub_$f" 120 "scripts/ubench/$f" ;;
     prof) run prof 1100 bash scripts/prof_round.sh "$tag" ;;
     py:*) f=${step#py:}; run "$(basename "$f" .py)" 600 python -u "$f" ;;
     tpy:*) f=${step#tpy:}; kv=""; case $f in *:*) kv=${f#*:}; f=${f%%:*};; esac
