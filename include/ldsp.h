@@ -79,7 +79,7 @@ int ldsp_debug_host_pools(size_t *total, size_t *idle);
  * fn: 0 exp, 1 log, 2 atan2(a, b), 3 tanh, 4 constrain (y as uint32 bits);
  * 5 exp, 6 log through the loops' fast paths (lm_*_loop); 7 atan2(a, b) in its
  * select-only form (lm_atan2f_vsel: the candidate evaluations of k_pll_seqc and
- * k_fm_pll).
+ * k_fm_pll); 8 constrain through v_fract (lm_constrain_fr: k_fm_pll's chain).
  * a, b, y are device pointers of n floats. */
 int ldsp_debug_math_eval(int fn, const float *a, const float *b, float *y, size_t n, void *stream);
 

@@ -1192,7 +1192,7 @@ int ldsp_stream_synchronize(void* stream)
 int ldsp_debug_math_eval(int fn, const float* a, const float* b, float* y, size_t n, void* stream)
 {
     return guard([&] {
-        LDSP_REQUIRE(fn >= 0 && fn <= 7, "math_eval: unknown function");
+        LDSP_REQUIRE(fn >= 0 && fn <= 8, "math_eval: unknown function");
         (void)current_device();
         k::math_eval(fn, a, b ? b : a, y, n, (hipStream_t)stream);
     });

@@ -736,6 +736,7 @@ __global__ void k_math_eval(int fn, const float* __restrict__ a, const float* __
     case 5: r = lm_expf_loop(a[i]); break;
     case 6: r = lm_logf_loop(a[i]); break;
     case 7: r = lm_atan2f_vsel(a[i], b[i]); break;
+    case 8: r = __uint_as_float(lm_constrain_fr(a[i])); break;
     default: break;
     }
     y[i] = r;

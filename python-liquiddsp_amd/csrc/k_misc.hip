@@ -64,7 +64,6 @@ __global__ void __launch_bounds__(256) k_freqdem(const float2* __restrict__ x, c
 // ------------------------------------------------------------------ FMStereo loop
 constexpr int kFmChunk = 4096;
 constexpr int kFmBatch = 4;      // samples per speculation batch
-constexpr int kFmCand = 16;      // candidate table indices per sample (64 lanes / kFmBatch)
 
 // One exact mixer step (demod.hpp:61-79; nco_crcf_mix_down with the 1024-entry
 // table):  (r1, i1) = (x + 0j) e^{-j theta};  pe = (float)(0.999 pe + 0.001 atan2(i1, r1));
@@ -87,95 +86,177 @@ __device__ __forceinline__ float fm_step(float x, const float* tab, uint32_t& th
 
 // The chain theta -> index -> atan2 -> pe -> C() -> theta is serial and does not
 // coalesce, but atan2 and the mixer output depend only on
-// the input sample and the table index.  So wave 0 runs the chain in batches of
-// kFmBatch samples and, beside batch b (in the same basic block, so the two
-// instruction streams interleave), evaluates atan2 and u for batch b + 1 at
-// kFmCand candidate indices per sample in its 64 lanes: indices around the
-// trajectory extrapolated from the state at batch b's start with the phase error
-// held (theta_h = theta + h (C(beta pe) + d) + C(alpha pe) h (h + 1) / 2).  The
-// chain step then only looks its index up (readlane) -- the same bits the direct
-// evaluation gives.  A batch in which some index falls outside its candidate
-// window (a few per thousand batches on FM composite signals,
-// scripts/analysis: fm_h2) is redone with the direct step from the saved state.
-// Waves 1-3 store chunk c - 1's l / r and stream chunk c + 1 of s into the LDS
-// double buffer while wave 0 walks chunk c.
-struct FmCand {
-    float z, u;          // this lane's atan2 and mixer output
-    uint32_t base;       // first candidate index of this lane's sample
+// the input sample and the table index.  So the chain runs in batches of
+// kFmBatch samples and only looks each step's index up among candidates
+// evaluated ahead of it -- the same bits the direct evaluation gives:
+//  * wave 0, the chain: at the start of batch g it publishes its state (theta,
+//    dtheta, pe) to an LDS ring, then takes batch g's candidates (read from LDS
+//    one batch ahead, into registers) and runs the 4 steps with readlane lookups;
+//  * waves 1 and 2, the helpers (one half of every batch's candidates each): for
+//    batch g they wait for the chain's state at batch g - 2, extrapolate the
+//    trajectory with the phase error held (theta_h = theta + h (C(beta pe) + d) +
+//    C(alpha pe) h (h + 1) / 2, h = 8..11 samples ahead) and evaluate atan2 and u
+//    at kFmNC indices around it for each of the batch's samples, then flag their
+//    half of the ring slot;
+//  * wave 3 stores chunk c - 1's l / r and streams chunk c + 1 of s into the
+//    LDS double buffer while the others work on chunk c.
+// A batch in which some index falls outside its window (~1 % of batches on FM
+// composite signals at this horizon) is redone with the direct step
+// from the saved state.  The hand-offs are LDS words with the batch number as a
+// tag (written after the data they guard; one wave's LDS accesses complete in
+// order), so no barrier sits inside a chunk.
+constexpr int kFmNC = 32;        // candidate indices per sample (the chain wave's two lane halves)
+static_assert(kFmNC == 32, "the chain evaluates C(alpha pe) and C(beta pe) of every candidate in one wave");
+constexpr int kFmRing = 8;       // batch slots of the hand-off rings
+constexpr int kFmHor = 2;        // batches between the state a helper extrapolates from and its batch
+
+struct FmBatchC {
+    double w[kFmBatch];          // sample j, candidate lane & 31: 0.001 * (double) atan2
+    float u[kFmBatch];           // and the mixer output
 };
 
-__device__ __forceinline__ FmCand fm_cands(const float* sp, int i0, int cnt, const float* tab, uint32_t theta,
-                                           uint32_t d, float pe, float alpha, float beta, int h0, int lane)
+// candidate e = j kFmNC + k (sample j of the batch, offset k from its base)
+__device__ __forceinline__ void fm_eval(const float* sp, int i0, int cnt, const float* tab, uint32_t base, int e,
+                                        float& z, float& u)
 {
-    const int j = lane / kFmCand;
-    const uint32_t h = (uint32_t)(h0 + j);
-    const uint32_t ca = lm_constrain(pe * alpha), cb = lm_constrain(pe * beta);
-    const uint32_t pred = theta + h * (cb + d) + ca * (h * (h + 1) / 2);
-    FmCand c;
-    c.base = (((pred + (1u << 21)) >> 22) - kFmCand / 2) & 0x3ffu;
-    const uint32_t idx = (c.base + (uint32_t)(lane % kFmCand)) & 0x3ffu;
-    const float x = sp[min(i0 + j, cnt - 1)];   // past the chunk's last batch: a value never used
+    const int j = e / kFmNC;
+    const uint32_t idx = (base + (uint32_t)(e % kFmNC)) & 0x3ffu;
+    const float x = sp[min(i0 + j, cnt - 1)];
     const float sn = tab[idx];
     const float cs = tab[(idx + 256) & 0x3ffu];
     const float r1 = x * cs - 0.0f * (-sn);
     const float i1 = x * (-sn) + 0.0f * cs;
-    c.z = lm_atan2f_vsel(i1, r1);
-    c.u = r1 * cs - i1 * (-sn);
-    return c;
+    z = lm_atan2f_vsel(i1, r1);
+    u = r1 * cs - i1 * (-sn);
 }
+
+__device__ __forceinline__ uint32_t fm_base(uint32_t theta, uint32_t d, float pe, float alpha, float beta, uint32_t h)
+{
+    const uint32_t ca = lm_constrain(pe * alpha), cb = lm_constrain(pe * beta);
+    const uint32_t pred = theta + h * (cb + d) + ca * (h * (h + 1) / 2);
+    return (((pred + (1u << 21)) >> 22) - kFmNC / 2) & 0x3ffu;
+}
+
+// Tags: one wave's LDS accesses execute in issue order, so a tag stored after its
+// data (or loaded before it) needs only the compiler kept from reordering them
+// (cbar), not a wait.
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
+__device__ __forceinline__ uint32_t lds_ld_u32(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st_u32(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
 __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, long n, FmState* st,
                                                 const float* __restrict__ table, float* __restrict__ lo,
                                                 float* __restrict__ ro)
 {
-    LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
     __shared__ float sb[2][kFmChunk + kFmBatch];
     __shared__ float ub[2][kFmChunk + 64];     // + 64: lanes 1..63 of wave 0 store their (identical) u here
+    // per slot and sample: 0.001 (double) atan2 at candidate k in entries k and k + 32
+    // (the chain's two lane halves), the mixer output at candidate k
+    __shared__ double cw[kFmRing][kFmBatch][64];
+    __shared__ float cu[kFmRing][kFmBatch][kFmNC];
+    __shared__ uint32_t cbase[kFmRing][kFmBatch];
+    __shared__ uint32_t crdy[kFmRing][2];     // per helper: batch g + 1 once its half of slot g % kFmRing holds batch g's candidates
+    __shared__ uint32_t sst[kFmRing][4];      // chain state at the start of batch g: theta, dtheta, pe, g + 1
     const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     for (int i = tid; i < 1024; i += 256) tab[i] = table[i];
+    for (int i = tid; i < kFmRing; i += 256) crdy[i][0] = crdy[i][1] = 0u, sst[i][3] = 0u;
     const long nch = (n + kFmChunk - 1) / kFmChunk;
     for (int i = tid; i < kFmChunk; i += 256) sb[0][i] = i < n ? s[i] : 0.0f;
     uint32_t theta = st->theta, d = st->dtheta;
     float pe = st->pe;
     const float alpha = st->alpha, beta = st->beta;
+    constexpr int kBpc = kFmChunk / kFmBatch;        // batches per full chunk
+#ifdef LDSP_TUNING
+    uint32_t n_miss = 0, n_late = 0, n_spin = 0, n_hwait = 0;
+#endif
     __syncthreads();
+    if (wave == 0) LDSP_LATENCY_CRITICAL();
     for (long c = 0; c <= nch; c++) {
         const int cur = (int)(c & 1);
-        if (tid < 64 && c < nch) {
-            const int lane = tid;
-            const long base = c * kFmChunk;
-            const int cnt = (int)min((long)kFmChunk, n - base);
-            const float* sp = sb[cur];
+        const long base = c * kFmChunk;
+        const int cnt = c < nch ? (int)min((long)kFmChunk, n - base) : 0;
+        const int nb = cnt / kFmBatch;
+        const uint32_t g0 = (uint32_t)(c * kBpc);     // call-wide number of the chunk's first batch
+        const float* sp = sb[cur];
+        if (wave == 0 && c < nch) {
             float* up = ub[cur];
-            const int nb = cnt / kFmBatch;
-            // lane 0 stores the chain's u; the other lanes store the same value past the chunk
-            const int uoff = lane == 0 ? 0 : kFmChunk + lane;
-            FmCand cc{};
-            if (nb > 0) cc = fm_cands(sp, 0, cnt, tab, theta, d, pe, alpha, beta, 0, lane);
+            const int uoff = lane == 0 ? 0 : kFmChunk + lane;   // lane 0 stores the chain's u
+            // lanes 0..31 form C(alpha pe), lanes 32..63 C(beta pe), of candidate lane & 31
+            const float mco = lane < 32 ? alpha : beta;
+            FmBatchC cc{}, nx{};
+            uint32_t cb4 = 0, nb4 = 0, ctag = 0, ntag = 0;
+            auto fetch = [&](uint32_t g, FmBatchC& v, uint32_t& b4, uint32_t& tag) {
+                const int sl = (int)(g % kFmRing);
+                const uint32_t t0 = lds_ld_u32(&crdy[sl][0]), t1 = lds_ld_u32(&crdy[sl][1]);
+                tag = t0 == t1 ? t0 : 0u;
+                cbar();
+#pragma unroll
+                for (int j = 0; j < kFmBatch; j++) {
+                    v.w[j] = cw[sl][j][lane];
+                    v.u[j] = cu[sl][j][lane & (kFmNC - 1)];
+                }
+                b4 = cbase[sl][lane & 3];
+            };
             for (int b = 0; b < nb; b++) {
+                const uint32_t g = g0 + (uint32_t)b;
                 const int i0 = b * kFmBatch;
-                // no branch around it: the candidates share a basic block with the chain steps
-                const FmCand nx = fm_cands(sp, i0 + kFmBatch, cnt, tab, theta, d, pe, alpha, beta, kFmBatch, lane);
+                if (lane == 0) {      // publish the state at this batch's start
+                    const int sl = (int)(g % kFmRing);
+                    sst[sl][0] = theta;
+                    sst[sl][1] = d;
+                    sst[sl][2] = __float_as_uint(pe);
+                    cbar();
+                    lds_st_u32(&sst[sl][3], g + 1u);
+                }
+                if (b == 0) fetch(g, cc, cb4, ctag);
+                else cc = nx, cb4 = nb4, ctag = ntag;
+#ifdef LDSP_TUNING
+                n_late += __builtin_amdgcn_readfirstlane(ctag) != g + 1u;
+#endif
+                while (__builtin_amdgcn_readfirstlane(ctag) != g + 1u) {   // not ready when prefetched
+                    __builtin_amdgcn_s_sleep(1);
+                    fetch(g, cc, cb4, ctag);
+#ifdef LDSP_TUNING
+                    n_spin++;
+#endif
+                }
                 const uint32_t th0 = theta, d0 = d;
                 const float pe0 = pe;
                 bool miss = false;
+                int u4 = 0;
 #pragma unroll
                 for (int j = 0; j < kFmBatch; j++) {
+                    // every candidate's step at once (the lanes): its pe and C(alpha pe) /
+                    // C(beta pe) -- the same operations as fm_step -- while the scalar
+                    // unit finds the true index; then the step is three readlanes
+                    const float pk = (float)(0.999 * (double)pe + cc.w[j]);
+                    const uint32_t ck = lm_constrain_fr(pk * mco);
                     const uint32_t idx = ((theta + (1u << 21)) >> 22) & 0x3ffu;
-                    const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)cc.base, j * kFmCand);
+                    const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)cb4, j);
                     const uint32_t off = (idx - bj) & 0x3ffu;
-                    miss |= off >= (uint32_t)kFmCand;
-                    const int ln = __builtin_amdgcn_readfirstlane(j * kFmCand + (int)(off & (kFmCand - 1)));
-                    const float z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.z), ln));
-                    const float u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.u), ln));
-                    pe = (float)(0.999 * (double)pe + 0.001 * (double)z);
-                    up[(i0 + j) * (lane == 0) + uoff] = u;
-                    d += lm_constrain(pe * alpha);
-                    theta += lm_constrain(pe * beta);
+                    miss |= off >= (uint32_t)kFmNC;
+                    const int ln = __builtin_amdgcn_readfirstlane((int)(off & (kFmNC - 1)));
+                    pe = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pk), ln));
+                    const uint32_t ca = (uint32_t)__builtin_amdgcn_readlane((int)ck, ln);
+                    const uint32_t cbt = (uint32_t)__builtin_amdgcn_readlane((int)ck, ln + 32);
+                    // u into lane j of u4, stored once per batch
+                    const int ub = __builtin_amdgcn_readlane(__float_as_int(cc.u[j]), ln);
+                    u4 = lane == j ? ub : u4;
+                    d += ca;
+                    theta += cbt;
                     theta += d;
+                    // the next batch's candidates, read while the last steps of this one run
+                    // (late enough for the helpers, early enough to hide the LDS latency)
+                    if (j == 1 && b + 1 < nb) fetch(g + 1u, nx, nb4, ntag);
                 }
-                if (miss) {      // an index left its window: redo the batch directly
+                if (!miss) {
+                    up[lane < kFmBatch ? i0 + lane : kFmChunk + lane] = __int_as_float(u4);
+                } else {         // an index left its window: redo the batch directly
+#ifdef LDSP_TUNING
+                    n_miss++;
+#endif
                     theta = th0;
                     d = d0;
                     pe = pe0;
@@ -184,22 +265,51 @@ __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, lon
                         up[(i0 + j) * (lane == 0) + uoff] = u;
                     }
                 }
-                cc = nx;
             }
             for (int i = nb * kFmBatch; i < cnt; i++) {
                 const float u = fm_step(sp[i], tab, theta, d, pe, alpha, beta);
                 up[i * (lane == 0) + uoff] = u;
             }
-        } else if (tid >= 64) {
+        } else if ((wave == 1 || wave == 2) && c < nch) {
+            // helper wave - 1: entries lane + 64 (wave - 1) of every batch of this chunk
+            const int hw = wave - 1;
+            const int e = lane + 64 * hw;
+            for (int b = 0; b < nb; b++) {
+                const uint32_t g = g0 + (uint32_t)b;
+                const uint32_t gs = g >= (uint32_t)kFmHor ? g - (uint32_t)kFmHor : 0u;   // state source batch
+                const int sl = (int)(gs % kFmRing);
+                while (__builtin_amdgcn_readfirstlane(lds_ld_u32(&sst[sl][3])) != gs + 1u) {
+#ifdef LDSP_TUNING
+                    n_hwait++;
+#endif
+                }
+                cbar();
+                const uint32_t th = sst[sl][0], dd = sst[sl][1];
+                const float pp = __uint_as_float(sst[sl][2]);
+                const uint32_t h0 = (g - gs) * (uint32_t)kFmBatch;
+                const int o = (int)(g % kFmRing);
+                const uint32_t bse = fm_base(th, dd, pp, alpha, beta, h0 + (uint32_t)(e / kFmNC));
+                float z, u;
+                fm_eval(sp, b * kFmBatch, cnt, tab, bse, e, z, u);
+                const int j = e / kFmNC, k = e % kFmNC;
+                const double w = 0.001 * (double)z;
+                cw[o][j][k] = w;
+                cw[o][j][k + 32] = w;
+                cu[o][j][k] = u;
+                if (k == 0) cbase[o][j] = bse;
+                cbar();
+                if (lane == 0) lds_st_u32(&crdy[o][hw], g + 1u);
+            }
+        } else if (wave == 3) {
             const int nxt = 1 - cur;        // holds chunk c - 1 (results) and receives chunk c + 1
-            const long pb = (c - 1) * kFmChunk, nb = (c + 1) * kFmChunk;
-            for (int i = tid - 64; i < kFmChunk; i += 192) {
+            const long pb = (c - 1) * kFmChunk, nbs = (c + 1) * kFmChunk;
+            for (int i = lane; i < kFmChunk; i += 64) {
                 if (c >= 1 && pb + i < n) {
                     const float x = sb[nxt][i], u = ub[nxt][i];
                     lo[pb + i] = x + u;
                     ro[pb + i] = x - u;
                 }
-                if (c + 1 < nch) sb[nxt][i] = nb + i < n ? s[nb + i] : 0.0f;
+                if (c + 1 < nch) sb[nxt][i] = nbs + i < n ? s[nbs + i] : 0.0f;
             }
         }
         __syncthreads();
@@ -209,6 +319,11 @@ __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, lon
         st->dtheta = d;
         st->pe = pe;
     }
+#ifdef LDSP_TUNING
+    if (lane == 0 && wave < 3)
+        printf("k_fm_pll wave %d: n %ld misses %u late %u spins %u helper_waits %u\n", wave, n, n_miss, n_late, n_spin,
+               n_hwait);
+#endif
 }
 
 __global__ void __launch_bounds__(256) k_interleave2(const float* __restrict__ a, const float* __restrict__ b, long n,

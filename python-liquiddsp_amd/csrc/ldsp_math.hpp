@@ -397,4 +397,26 @@ __host__ __device__ inline uint32_t lm_constrain(float theta)
     return v >= 4294967296.0f ? 0u : (uint32_t)v;
 }
 
+// lm_constrain with the fraction from v_fract (p - floor(p), which the hardware
+// keeps below 1): for p >= 0 that is p - trunc(p); for p < 0 it is the exact
+// p - trunc(p) + 1 rounded once, as the reference's double add then float
+// rounding gives, except where that rounds to 1.0 -- p in [-2^-25, 0), where
+// the reference's fpart * 2^32 = 2^32 wraps to 0 and v_fract gives 1 - 2^-24:
+// those p return 0 explicitly.  Bitwise to lm_constrain (ldsp_debug_math_eval
+// fn 8 vs 4 in tests/test_gpu_parity.py), four operations shorter.  (The host
+// form states v_fract's definition; only the device one is used.)
+__host__ __device__ inline uint32_t lm_constrain_fr(float theta)
+{
+    const float p = (float)((double)theta * 0.159154943091895);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float fr = __builtin_amdgcn_fractf(p);
+#else
+    const float fr = fminf(p - floorf(p), 0x1.fffffep-1f);
+#endif
+    const uint32_t v = (uint32_t)(fr * 4294967296.0f);
+    uint32_t pb;
+    __builtin_memcpy(&pb, &p, 4);
+    return pb - 0x80000001u <= 0x32FFFFFFu ? 0u : v;
+}
+
 } // namespace ldsp

@@ -91,6 +91,24 @@ def test_device_math_bitwise(ld, ora, rng):
     got = ty.cpu().numpy().view(np.uint32)
     ref = np.array([ora.constrain(float(t)) for t in th], np.uint32)
     assert np.array_equal(got, ref)
+    # fn 8, constrain through v_fract (k_fm_pll's chain), against fn 4 on the device:
+    # random angles, and every 16th theta whose p = theta / 2 pi lies around the
+    # [-2^-25, 0) range where p - floor(p) rounds to 1.0 (both signs), zeros,
+    # integers of turns and their neighbours
+    edge = np.arange(0xB3000000, 0xB5000000, 16, dtype=np.uint32).view(np.float32)
+    turns = np.float32(2 * np.pi) * np.float32(np.arange(-40, 41))
+    near = np.concatenate([np.nextafter(turns, np.float32(np.inf)), np.nextafter(turns, np.float32(-np.inf)), turns])
+    th8 = np.ascontiguousarray(np.concatenate([np.float32(rng.uniform(-20, 20, 1 << 18)), edge, -edge, near,
+                                               np.float32([0.0, -0.0, 1e-30, -1e-30, 3e-45, -3e-45])]))
+    ta = torch.from_numpy(th8).cuda()
+    y4, y8 = torch.empty_like(ta), torch.empty_like(ta)
+    ld._math_eval(4, ta.data_ptr(), ta.data_ptr(), y4.data_ptr(), th8.size, 0)
+    ld._math_eval(8, ta.data_ptr(), ta.data_ptr(), y8.data_ptr(), th8.size, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(y4.view(torch.int32), y8.view(torch.int32))
+    sub = th8[-4096:]
+    assert np.array_equal(y8.cpu().numpy()[-4096:].view(np.uint32),
+                          np.array([ora.constrain(float(t)) for t in sub], np.uint32))
 
 
 # ------------------------------------------------------------------ FIR
