@@ -1,6 +1,7 @@
 """AmpModem carrier loop of short calls: k_pll_seqc (k_pll.hip), used for calls
-below 2 048 PCM samples in carrier mode (the README's 65 536-sample SDR block
-gives 1 573).  Reference: ampmodem_demodulate_block behind
+below 1 024 PCM samples in carrier mode (from round 5; longer calls, the
+README's 65 536-sample SDR block with its 1 573 included, take the candidates +
+walk path, so the sizes around the threshold check both sides).  Reference: ampmodem_demodulate_block behind
 /root/reference/src/demod.hpp:290-296 (AmpModem(carrier=True) ->
 ampmodem_demod_dsb_pll_carrier).
 
@@ -18,7 +19,7 @@ from conftest import cgauss
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [1, 3, 4, 5, 1573, 2047]
+SIZES = [1, 3, 4, 5, 1023, 1024, 1573, 2047]
 
 
 def assert_bitwise(y, ref):
@@ -83,11 +84,11 @@ def test_seqc_noise_window_misses(ld, ora, rng):
     """Pure noise: the loop never locks, the extrapolated index misses its
     16-cell window often, and those batches are redone directly."""
     x = cgauss(rng, 30_000)
-    y, ref, g, o = _run_calls(ld, ora, x, [1573])
+    y, ref, g, o = _run_calls(ld, ora, x, [1000])
     assert_bitwise(y, ref)
     assert g.pll_state() == o.pll_state
     batches, redone = g._seq_stats()
-    assert batches == sum(min(1573, len(x) - a) // 4 for a in range(0, len(x), 1573))
+    assert batches == sum(min(1000, len(x) - a) // 4 for a in range(0, len(x), 1000))
     assert redone > 0, "the window-miss redo path did not run"
 
 
