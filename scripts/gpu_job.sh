@@ -9,6 +9,8 @@
 #   b20 / b100  bench.py at the driver setting (20 steps, 5 warm-up) / 100 steps, no components
 #   b20nk       the same 20 steps without per-kernel HIP events in the timed steps
 #   bench       bench.py with every component and the CPU baseline (the round-end line)
+#   bench20     the same at the driver setting (20 steps, 5 warm-up)
+#   pmccopy     this job's prof summary into profiles/ (so the bench lines after it cite it)
 #   tl20        tuning build, 20 steps, LDSP_PROF_TIMELINE dump + scripts/prof_timeline.py
 #   chains      scripts/chains_bench.py
 #   channels    scripts/channels_run.py (8 AMRadio chains on one GPU)
@@ -43,6 +45,8 @@ for step in "$@"; do
     b20nk) run b20nk 400 $B --steps 20 --warmup 5 --no-kprof ;;
     b100) run b100 400 $B --steps 100 ;;
     bench) run bench 900 python -u bench.py ;;
+    bench20) run bench20 900 python -u bench.py --steps 20 --warmup 5 ;;
+    pmccopy) cp "gpurun_out/prof/$tag/summary.json" "profiles/${tag}_pmc_summary.json" && echo "[pmccopy] profiles/${tag}_pmc_summary.json" ;;
     tl20|tl20:*) kv=${step#tl20}; kv=${kv#:}; name="tl20$(echo "_$kv" | tr ',=' '_-')"; rm -f "$o/$name.txt"
           env $(echo "$kv" | tr ',' ' ') LDSP_PKG_DIR=build_tuning LDSP_PROF_TIMELINE="$o/$name.txt" \
             timeout -k 10 400 $B --steps 20 --warmup 5 --no-kprof > "$o/$name.log" 2>&1
