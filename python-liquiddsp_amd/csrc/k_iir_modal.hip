@@ -216,6 +216,12 @@ __device__ __forceinline__ void modal_scan(const IirModalCoef& cf, const double*
                 E.w0[k] = w;
             }
         }
+        // the states of every section materialised after each pair: keeps the
+        // recursion sample-major (the compiler otherwise runs it section by section,
+        // interleaved with the scan, and holds all 32 converted samples: 123 -> 89
+        // VGPRs, same time, r05z)
+#pragma unroll
+        for (int k = 0; k < M; k++) asm volatile("" : "+v"(E.w0[k]), "+v"(E.w1[k]));
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
