@@ -232,7 +232,11 @@ __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, lon
                     // C(beta pe) -- the same operations as fm_step -- while the scalar
                     // unit finds the true index; then the step is three readlanes
                     const float pk = (float)(0.999 * (double)pe + cc.w[j]);
-                    const uint32_t ck = lm_constrain_fr(pk * mco);
+                    uint32_t ck = lm_constrain_fr(pk * mco);
+                    // formed here, as soon as pe is known: the compiler otherwise pairs it
+                    // with the next step's (packed f32 ops), which puts that step's pe on
+                    // this step's path to its index
+                    asm volatile("" : "+v"(ck));
                     const uint32_t idx = ((theta + (1u << 21)) >> 22) & 0x3ffu;
                     const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)cb4, j);
                     const uint32_t off = (idx - bj) & 0x3ffu;
