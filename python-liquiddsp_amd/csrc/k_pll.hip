@@ -848,16 +848,37 @@ struct WState {
 
 // Generic walk of every sample in [sa, sb] (the samples of one lane-block's
 // entries and the gaps between them): 64 consecutive samples per step, the
-// candidate phases and offset model of up to kFbPre steps loaded up front (one
-// memory round trip for a whole lane-block's range instead of one per step),
-// each repair applied at the true index.  A repair at one of the lane-block's
-// entries that crosses the one cell its entry record allows (E1) takes that
-// record's kick differences and output (the same pll_eval k_pll_entries ran);
-// any other one (a gap sample, or two or more cells) loads its loop inputs and
+// candidate records, offset model and loop inputs of kFbPre steps loaded up front
+// into registers (one memory round trip for a whole lane-block's range instead of
+// one per step and per full repair), each repair applied at the true index.  A
+// repair at one of the lane-block's entries that crosses the one cell its entry
+// record allows (E1) takes that record's kick differences and output (the same
+// pll_eval k_pll_entries ran); any other one (a gap sample, or two or more cells)
 // evaluates the loop step in full against the candidate's recorded kicks.  Used
 // where the sparse walk cannot prove a gap clean, and for every lane-block in
 // the LDSP_DEBUG_PLL=2 check (which evaluates every repair in full).
-constexpr int kFbPre = 16;
+constexpr int kFbPre = 4;      // 64-sample steps loaded up front (a lane-block's range is ~4)
+
+struct FbKick {
+    uint32_t dk1, dk2p, out;
+};
+// walk_fallback's rare full loop step (kept out of line: inlined, its code and
+// registers made every repair of the loop around it ~150 instructions long)
+__device__ __noinline__ FbKick fb_full_step(const float* tab, uint32_t wj, uint32_t cell, uint4 rec, float2 u0v,
+                                            float2 u1v, int j, uint32_t rrel, FullCtx fc)
+{
+    const float2 u0 = make_float2(__uint_as_float(rl(__float_as_uint(u0v.x), j)),
+                                  __uint_as_float(rl(__float_as_uint(u0v.y), j)));
+    const float2 u1 = make_float2(__uint_as_float(rl(__float_as_uint(u1v.x), j)),
+                                  __uint_as_float(rl(__float_as_uint(u1v.y), j)));
+    const Kick kt = pll_eval(tab, ((wj >> 22) + cell) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas,
+                             fc.out_idx);
+    FbKick r;
+    r.dk1 = rfl(kt.k1 - rl(rec.y, j));
+    r.dk2p = rfl(kt.k2 - rl(rec.z, j)) - rrel * r.dk1;
+    r.out = rfl(__float_as_uint(kt.out));
+    return r;
+}
 
 __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_t S, CandBuf cb, FullCtx fc,
                                              const float* tab, float* y, int lane, uint32_t esrel, uint32_t edk1,
@@ -865,56 +886,65 @@ __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_
 {
     const unsigned long long emask = nv >= 64 ? ~0ull : nv <= 0 ? 0ull : ((1ull << nv) - 1ull);
     const bool use_e1 = cb.dbg != 2;
-    const uint32_t* recw = (const uint32_t*)cb.rec;          // word 0 of record s: recw[4 s]
     for (long b0 = sa; b0 <= sb; b0 += 64l * kFbPre) {
-        uint32_t W[kFbPre], A[kFbPre];
+        // every input of kFbPre steps in registers before the first: the record
+        // (candidate phase word, kicks), the offset model and the full step's two
+        // samples -- a repair that needs the full loop step reads them lane by lane.
+        // (Fully unrolled with guards, not a break: a loop-indexed array would live
+        // in scratch memory.)
+        uint4 R[kFbPre];
+        uint32_t A[kFbPre];
+        float2 U0[kFbPre], U1[kFbPre];
 #pragma unroll
         for (int q = 0; q < kFbPre; q++) {
             const long s = min(b0 + 64l * q + lane, sb);
-            W[q] = recw[4 * s];
+            R[q] = cb.rec[s];
             const long k = s / kCand;
             A[q] = cb.pth[k] + (uint32_t)s * cb.pd[k];
+            U0[q] = fc.x0[s];
+            const long gi = s - fc.m;
+            U1[q] = gi >= 0 ? fc.x[gi] : fc.hist[gi + fc.m];
         }
 #pragma unroll
         for (int q = 0; q < kFbPre; q++) {
             const long base = b0 + 64l * q;
-            if (base > sb) break;
-            const unsigned long long M = __builtin_amdgcn_ballot_w64(base + lane <= sb);
-            const uint32_t srel = (uint32_t)(base + lane - (long)S);
-            uint32_t v = (W[q] & 0x3fffffu) + g.Kb + srel * g.D + A[q];
-            unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
-            while (mask != 0) {
-                const int j = __builtin_ctzll(mask);
-                const uint32_t vj = rl(v, j), wj = rl(W[q], j);
-                const uint32_t rrel = (uint32_t)j + (uint32_t)(base - (long)S);
-                const uint32_t cell = vj >> 22;            // true index - candidate's (mod 1024)
-                const unsigned long long em = __builtin_amdgcn_ballot_w64(esrel == rrel) & emask;
-                uint32_t dk1, dk2p, out;
-                if (use_e1 && em != 0 && cell == ((wj & 0x3fffffu) >= (1u << 21) ? 1u : 1023u)) {
-                    const int L = __builtin_ctzll(em);
-                    dk1 = rl(edk1, L);
-                    dk2p = rl(edk2p, L);                  // dk2 - srel dk1
-                    out = rl(eout, L);
-                } else {
-                    // the loop step at the true index (any number of cells from the
-                    // candidate's), evaluated in full; the candidate's kicks from its record
-                    const long s = base + j;
-                    const uint4 r0 = cb.rec[s];
-                    const float2 u0 = fc.x0[s];
-                    const long gi = s - fc.m;
-                    const float2 u1 = gi >= 0 ? fc.x[gi] : fc.hist[gi + fc.m];
-                    const Kick kt = pll_eval(tab, ((wj >> 22) + cell) & 0x3ffu, u0, u1, fc.alpha, fc.beta,
-                                             fc.mod_index, fc.costas, fc.out_idx);
-                    dk1 = rfl(kt.k1 - r0.y);
-                    dk2p = rfl(kt.k2 - r0.z) - rrel * dk1;
-                    out = rfl(__float_as_uint(kt.out));
+            if (base <= sb) {
+                const unsigned long long M = __builtin_amdgcn_ballot_w64(base + lane <= sb);
+                const uint32_t srel = (uint32_t)(base + lane - (long)S);
+                uint32_t v = (R[q].x & 0x3fffffu) + g.Kb + srel * g.D + A[q];
+                unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
+                // the step's repaired outputs: lane j of yv, stored once after the step
+                uint32_t yv = 0;
+                unsigned long long rep = 0;
+                while (mask != 0) {
+                    const int j = __builtin_ctzll(mask);
+                    const uint32_t vj = rl(v, j), wj = rl(R[q].x, j);
+                    const uint32_t rrel = (uint32_t)j + (uint32_t)(base - (long)S);
+                    const uint32_t cell = vj >> 22;            // true index - candidate's (mod 1024)
+                    const unsigned long long em = __builtin_amdgcn_ballot_w64(esrel == rrel) & emask;
+                    uint32_t dk1, dk2p, out;
+                    if (use_e1 && em != 0 && cell == ((wj & 0x3fffffu) >= (1u << 21) ? 1u : 1023u)) {
+                        const int L = __builtin_ctzll(em);
+                        dk1 = rl(edk1, L);
+                        dk2p = rl(edk2p, L);                  // dk2 - srel dk1
+                        out = rl(eout, L);
+                    } else {
+                        // the loop step at the true index (any number of cells from the
+                        // candidate's), evaluated in full; the candidate's kicks from its record
+                        const FbKick fk = fb_full_step(tab, wj, cell, R[q], U0[q], U1[q], j, rrel, fc);
+                        dk1 = fk.dk1;
+                        dk2p = fk.dk2p;
+                        out = fk.out;
+                    }
+                    yv = lane == j ? out : yv;
+                    rep |= 1ull << j;
+                    g.Kb += dk2p;
+                    g.D += dk1;
+                    g.nrep++;
+                    v += dk2p + srel * dk1;
+                    mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M & ((~0ull << j) << 1);
                 }
-                if (lane == 0) y[base + j] = __uint_as_float(out);
-                g.Kb += dk2p;
-                g.D += dk1;
-                g.nrep++;
-                v += dk2p + srel * dk1;
-                mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M & ((~0ull << j) << 1);
+                if ((rep >> lane) & 1ull) y[base + lane] = __uint_as_float(yv);
             }
         }
     }
