@@ -109,6 +109,7 @@ constexpr int kFmNC = 32;        // candidate indices per sample (the chain wave
 static_assert(kFmNC == 32, "the chain evaluates C(alpha pe) and C(beta pe) of every candidate in one wave");
 constexpr int kFmRing = 8;       // batch slots of the hand-off rings
 constexpr int kFmHor = 2;        // batches between the state a helper extrapolates from and its batch
+constexpr uint64_t kFmWaitTicks = 2000;   // 20 us of s_memrealtime: a hand-off that late is given up (exactly)
 
 struct FmBatchC {
     double w[kFmBatch];          // sample j, candidate lane & 31: 0.001 * (double) atan2
@@ -215,16 +216,24 @@ __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, lon
 #ifdef LDSP_TUNING
                 n_late += __builtin_amdgcn_readfirstlane(ctag) != g + 1u;
 #endif
-                while (__builtin_amdgcn_readfirstlane(ctag) != g + 1u) {   // not ready when prefetched
-                    __builtin_amdgcn_s_sleep(1);
-                    fetch(g, cc, cb4, ctag);
+                bool miss = false;
+                if (__builtin_amdgcn_readfirstlane(ctag) != g + 1u) {   // not ready when prefetched
+                    const uint64_t tw = wall_clock64();
+                    do {
+                        // no helper within kFmWaitTicks: the batch is stepped directly (exact either way)
+                        if (wall_clock64() - tw > kFmWaitTicks) {
+                            miss = true;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        fetch(g, cc, cb4, ctag);
 #ifdef LDSP_TUNING
-                    n_spin++;
+                        n_spin++;
 #endif
+                    } while (__builtin_amdgcn_readfirstlane(ctag) != g + 1u);
                 }
                 const uint32_t th0 = theta, d0 = d;
                 const float pe0 = pe;
-                bool miss = false;
                 int u4 = 0;
 #pragma unroll
                 for (int j = 0; j < kFmBatch; j++) {
@@ -282,10 +291,19 @@ __global__ void __launch_bounds__(256) k_fm_pll(const float* __restrict__ s, lon
                 const uint32_t g = g0 + (uint32_t)b;
                 const uint32_t gs = g >= (uint32_t)kFmHor ? g - (uint32_t)kFmHor : 0u;   // state source batch
                 const int sl = (int)(gs % kFmRing);
-                while (__builtin_amdgcn_readfirstlane(lds_ld_u32(&sst[sl][3])) != gs + 1u) {
+                if (__builtin_amdgcn_readfirstlane(lds_ld_u32(&sst[sl][3])) != gs + 1u) {
+                    const uint64_t tw = wall_clock64();
+                    bool late = false;
+                    do {
 #ifdef LDSP_TUNING
-                    n_hwait++;
+                        n_hwait++;
 #endif
+                        if (wall_clock64() - tw > kFmWaitTicks) {   // the chain steps this batch directly
+                            late = true;
+                            break;
+                        }
+                    } while (__builtin_amdgcn_readfirstlane(lds_ld_u32(&sst[sl][3])) != gs + 1u);
+                    if (late) continue;
                 }
                 cbar();
                 const uint32_t th = sst[sl][0], dd = sst[sl][1];
