@@ -583,6 +583,111 @@ __device__ __forceinline__ void k_agc_runfix_body(const float2* __restrict__ x, 
         gs[7] = r.timer;
     }
 }
+// The same repair with one wave per run (C a multiple of 8 x 64): chunk m of
+// the run is split into 64 segments of C / 64 samples; lane j brings the run's
+// true state to its segment by the approximate loop (from the input staged in
+// LDS: the small-call technique, which from a true state tracks the exact
+// trajectory bit for bit almost always) and runs its segment exactly; a lane
+// whose start differs from its left neighbour's exact end is re-run by lane 0
+// from that end, in order.  A chunk costs ~C approximate + C / 64 exact steps
+// of latency instead of C exact ones; the checkpoints, records, stop rules and
+// outputs are those of k_agc_runfix.
+struct AgcLdsX {                 // absolute sample index -> the chunk staged in LDS
+    const float2* xs;
+    long base;
+    __device__ __forceinline__ float2 operator[](long i) const { return xs[i - base]; }
+};
+__device__ __forceinline__ bool agc_reg_eq(const AgcReg& a, const AgcReg& b)
+{
+    return __float_as_uint(a.g) == __float_as_uint(b.g) && __float_as_uint(a.y2p) == __float_as_uint(b.y2p) &&
+           a.mode == b.mode && a.timer == b.timer;
+}
+__device__ __forceinline__ AgcReg agc_reg_shfl(const AgcReg& e, int src)
+{
+    return AgcReg{__shfl(e.g, src), __shfl(e.y2p, src), __shfl(e.mode, src), __shfl(e.timer, src)};
+}
+__device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict__ x, long n, const AgcState* st,
+                                                        int C, long nch, unsigned* __restrict__ sc,
+                                                        const unsigned long long* __restrict__ flags,
+                                                        float2* __restrict__ y, uint8_t* __restrict__ status,
+                                                        unsigned* dbg, unsigned* cp)
+{
+    LDSP_LATENCY_CRITICAL();
+    extern __shared__ float2 xs[];
+    const long k = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (k >= nch || !agc_flag(flags, k) || (k > 0 && agc_flag(flags, k - 1))) return;
+    const AgcState p = *st;
+    const int seg = C / 64;
+    AgcReg T{__uint_as_float(pred_word(sc, st, k, 0)), __uint_as_float(pred_word(sc, st, k, 1)),
+             (int)pred_word(sc, st, k, 2), pred_word(sc, st, k, 3)};
+    bool inrun = true;
+    for (long m = k; m < nch; m++) {
+        unsigned* gs = sc + m * 8;
+        if (m > k) {
+            const bool b = agc_flag(flags, m);
+            if (!(inrun && b)) {
+                if (b) break;                               // the next run's start
+                inrun = false;
+                if (ldntu(gs) == __float_as_uint(T.g) && ldntu(gs + 1) == __float_as_uint(T.y2p) &&
+                    ldntu(gs + 2) == (unsigned)T.mode && ldntu(gs + 3) == T.timer)
+                    break;                                  // coalesced with the stored trajectory
+            }
+        }
+        const long s0 = m * C, s1 = min(n, s0 + C);
+        const int cnt = (int)(s1 - s0);
+        if (lane == 0) {
+            if (dbg) atomicAdd(dbg, 1u);
+            atomicAdd((unsigned*)&st->pad[2], 1u);          // ldsp_debug_agc_reruns (runfix)
+            gs[0] = __float_as_uint(T.g);
+            gs[1] = __float_as_uint(T.y2p);
+            gs[2] = (unsigned)T.mode;
+            gs[3] = T.timer;
+        }
+        __syncthreads();                                    // the previous chunk's reads of xs are done
+        for (int i = lane; i < cnt; i += 64) xs[i] = x[s0 + i];
+        __syncthreads();
+        const AgcLdsX xl{xs, s0};
+        const long a = min(s1, s0 + (long)lane * seg), b = min(s1, a + seg);
+        AgcReg r = T;
+        agc_run_approx(r, p, xl, s0, a);
+        AgcReg S = r;                                       // this segment's start (a guess for lane > 0)
+        agc_run<true>(r, p, xl, a, b, y, status);
+        // lanes whose start is not their left neighbour's exact end: re-run in order
+        // (the shuffles on every lane: a lane reading an inactive one gets garbage)
+        AgcReg pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
+        uint64_t bad = __ballot(lane >= 1 && a < b && !agc_reg_eq(S, pe));
+        while (bad) {
+            const int j = __builtin_ctzll(bad);
+            const AgcReg e = agc_reg_shfl(r, j - 1);
+            AgcReg f = e;
+            if (lane == 0) agc_run<true>(f, p, xl, s0 + (long)j * seg, min(s1, s0 + (long)j * seg + seg), y, status);
+            f = agc_reg_shfl(f, 0);
+            if (lane == j) {
+                S = e;
+                r = f;
+            }
+            pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
+            bad = __ballot(lane > j && a < b && !agc_reg_eq(S, pe));
+        }
+        // the true states at the checkpoints inside the chunk (offsets 64 (q + 1) < cnt)
+        if (cp && lane > 0 && (lane * seg) % kAgcCp == 0 && (long)lane * seg < cnt) {
+            unsigned* c = cp + m * (C / kAgcCp) * 4 + ((lane * seg) / kAgcCp - 1) * 4;
+            c[0] = __float_as_uint(S.g);
+            c[1] = __float_as_uint(S.y2p);
+            c[2] = (unsigned)S.mode;
+            c[3] = S.timer;
+        }
+        T = agc_reg_shfl(r, (cnt - 1) / seg);              // the chunk's true end state
+        if (lane == 0) {
+            gs[4] = __float_as_uint(T.g);
+            gs[5] = __float_as_uint(T.y2p);
+            gs[6] = (unsigned)T.mode;
+            gs[7] = T.timer;
+        }
+    }
+}
+
 struct AgcRunfixArgs {
     const float2* x;
     long n;
@@ -598,6 +703,8 @@ struct AgcRunfixArgs {
 };
 __device__ __forceinline__ void k_agc_runfix_run(const AgcRunfixArgs& a) { k_agc_runfix_body(a.x, a.n, a.st, a.C, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
 LDSP_KERNEL_PAIR(k_agc_runfix, AgcRunfixArgs, k_agc_runfix_run, 64)
+__device__ __forceinline__ void k_agc_runfix_wide_run(const AgcRunfixArgs& a) { k_agc_runfix_wide_body(a.x, a.n, a.st, a.C, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
+LDSP_KERNEL_PAIR(k_agc_runfix_wide, AgcRunfixArgs, k_agc_runfix_wide_run, 64)
 
 
 // Parallel pre-check: bit c of flags[c / 64] = chunk c's start state differs
@@ -765,6 +872,13 @@ static unsigned* agc_cp(const SpecPlan& p)
                                                                       : nullptr;
 }
 
+// the one-wave-per-run repair (k_agc_runfix_wide) for the large chunk-parallel calls
+static bool agc_runfix_wide(const SpecPlan& p)
+{
+    static const bool on = LDSP_KNOB("LDSP_AGC_WIDE", 1) != 0;     // tuning build: A/B against k_agc_runfix
+    return on && !(p.tsa & 3) && p.C % 64 == 0 && p.C >= 64 && p.C <= 4096;
+}
+
 void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
@@ -787,10 +901,14 @@ static void agc_rounds(const void* x, size_t n, AgcState* st, const SpecPlan& p,
         launch("k_agc_flags", k_agc_flags, k_agc_flags_many, dim3(nb), dim3(64), 0, s,
                AgcFlagsArgs{p.C, p.W, p.nchunks, (const unsigned*)p.scratch, (const AgcState*)st, spec, flags});
         if (round == p.rounds) break;
-        launch("k_agc_runfix", k_agc_runfix, k_agc_runfix_many, dim3(nb), dim3(64), 0, s,
-               AgcRunfixArgs{(const float2*)x, (long)n, (const AgcState*)st, p.C, p.nchunks, (unsigned*)p.scratch,
-                             (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr,
-                             agc_cp(p)});
+        const AgcRunfixArgs ra{(const float2*)x, (long)n, (const AgcState*)st, p.C, p.nchunks, (unsigned*)p.scratch,
+                               (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr,
+                               agc_cp(p)};
+        if (agc_runfix_wide(p))
+            launch("k_agc_runfix", k_agc_runfix_wide, k_agc_runfix_wide_many, dim3((unsigned)p.nchunks), dim3(64),
+                   (size_t)p.C * sizeof(float2), s, ra);
+        else
+            launch("k_agc_runfix", k_agc_runfix, k_agc_runfix_many, dim3(nb), dim3(64), 0, s, ra);
     }
 }
 
