@@ -2160,11 +2160,16 @@ int ldsp_agc_execute(ldsp_agc_t q, const void* x, size_t n, void* y, uint8_t* st
         const void* dx = q->stg.dev_in(e, x, n * 8);
         void* dy = q->stg.dev_out(e, y, n * 8);
         uint8_t* dstat = status ? (uint8_t*)q->status.ensure(std::max<size_t>(n, 1), q->device) : nullptr;
-        // exact warm-up W = 20/bandwidth after an approximate one of Wa = 40/bandwidth
+        // exact warm-up W = 5/bandwidth after an approximate one of Wa = 40/bandwidth
         // (k_agc.hip); measured on the AM chain at bandwidth 0.01 the exact loop then
-        // coalesces within ~110 samples on average, 2834 at worst.
+        // coalesces within ~110 samples on average, 2834 at worst.  The chunks that
+        // have not by then (~70 of 1 573 per 64 Mi call at W = 5/bw, 7 at 20/bw) go
+        // to the windowed one-wave run-fix, which stops at the first checkpoint that
+        // meets the stored trajectory: single call 3.72 -> 3.42 ms against W = 20/bw
+        // (W = 3/bw: 3.71, more runs), 20-step and batched channels unchanged
+        // (gpurun_out r05zo).
         const float a = q->h.alpha > 1e-6f ? q->h.alpha : 1e-6f;
-        static const float wmul = LDSP_KNOB_F("LDSP_AGC_WMUL", 20.0f);
+        static const float wmul = LDSP_KNOB_F("LDSP_AGC_WMUL", 5.0f);
         static const float wamul = LDSP_KNOB_F("LDSP_AGC_WAMUL", 40.0f);
         // repair rounds (flag + run-by-run re-run launches) before the one-wave
         // verifier, which re-runs whatever a round left: on the bench chain every

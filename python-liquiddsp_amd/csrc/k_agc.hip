@@ -583,15 +583,19 @@ __device__ __forceinline__ void k_agc_runfix_body(const float2* __restrict__ x, 
         gs[7] = r.timer;
     }
 }
-// The same repair with one wave per run (C a multiple of 8 x 64): chunk m of
-// the run is split into 64 segments of C / 64 samples; lane j brings the run's
-// true state to its segment by the approximate loop (from the input staged in
+// The same repair with one wave per run: chunk m of the run is processed in
+// windows of 64 segments of `seg` samples; lane j brings the window's true
+// start state to its segment by the approximate loop (from the chunk staged in
 // LDS: the small-call technique, which from a true state tracks the exact
 // trajectory bit for bit almost always) and runs its segment exactly; a lane
 // whose start differs from its left neighbour's exact end is re-run by lane 0
-// from that end, in order.  A chunk costs ~C approximate + C / 64 exact steps
-// of latency instead of C exact ones; the checkpoints, records, stop rules and
-// outputs are those of k_agc_runfix.
+// from that end, in order.  After each window the true states at the chunk's
+// checkpoints in it are compared with the stored ones: at the first match the
+// stored trajectory from there on is the true one (outputs, later checkpoints,
+// end state), so the chunk is done -- a chunk costs ~min(coalescence, C)
+// approximate + seg exact steps per window instead of its coalescence time in
+// exact steps.  Records, checkpoints, stop rules and outputs are those of
+// k_agc_runfix.
 struct AgcLdsX {                 // absolute sample index -> the chunk staged in LDS
     const float2* xs;
     long base;
@@ -607,7 +611,7 @@ __device__ __forceinline__ AgcReg agc_reg_shfl(const AgcReg& e, int src)
     return AgcReg{__shfl(e.g, src), __shfl(e.y2p, src), __shfl(e.mode, src), __shfl(e.timer, src)};
 }
 __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict__ x, long n, const AgcState* st,
-                                                        int C, long nch, unsigned* __restrict__ sc,
+                                                        int C, int seg, long nch, unsigned* __restrict__ sc,
                                                         const unsigned long long* __restrict__ flags,
                                                         float2* __restrict__ y, uint8_t* __restrict__ status,
                                                         unsigned* dbg, unsigned* cp)
@@ -618,10 +622,13 @@ __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict_
     const int lane = threadIdx.x;
     if (k >= nch || !agc_flag(flags, k) || (k > 0 && agc_flag(flags, k - 1))) return;
     const AgcState p = *st;
-    const int seg = C / 64;
     AgcReg T{__uint_as_float(pred_word(sc, st, k, 0)), __uint_as_float(pred_word(sc, st, k, 1)),
              (int)pred_word(sc, st, k, 2), pred_word(sc, st, k, 3)};
     bool inrun = true;
+#ifdef LDSP_AGC_TRACE
+    const long t_start = wall_clock64();
+    int n_chunks = 0, n_rep = 0, n_win = 0;
+#endif
     for (long m = k; m < nch; m++) {
         unsigned* gs = sc + m * 8;
         if (m > k) {
@@ -636,6 +643,7 @@ __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict_
         }
         const long s0 = m * C, s1 = min(n, s0 + C);
         const int cnt = (int)(s1 - s0);
+        unsigned* cpm = cp ? cp + m * (C / kAgcCp) * 4 : nullptr;
         if (lane == 0) {
             if (dbg) atomicAdd(dbg, 1u);
             atomicAdd((unsigned*)&st->pad[2], 1u);          // ldsp_debug_agc_reruns (runfix)
@@ -648,44 +656,73 @@ __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict_
         for (int i = lane; i < cnt; i += 64) xs[i] = x[s0 + i];
         __syncthreads();
         const AgcLdsX xl{xs, s0};
-        const long a = min(s1, s0 + (long)lane * seg), b = min(s1, a + seg);
-        AgcReg r = T;
-        agc_run_approx(r, p, xl, s0, a);
-        AgcReg S = r;                                       // this segment's start (a guess for lane > 0)
-        agc_run<true>(r, p, xl, a, b, y, status);
-        // lanes whose start is not their left neighbour's exact end: re-run in order
-        // (the shuffles on every lane: a lane reading an inactive one gets garbage)
-        AgcReg pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
-        uint64_t bad = __ballot(lane >= 1 && a < b && !agc_reg_eq(S, pe));
-        while (bad) {
-            const int j = __builtin_ctzll(bad);
-            const AgcReg e = agc_reg_shfl(r, j - 1);
-            AgcReg f = e;
-            if (lane == 0) agc_run<true>(f, p, xl, s0 + (long)j * seg, min(s1, s0 + (long)j * seg + seg), y, status);
-            f = agc_reg_shfl(f, 0);
-            if (lane == j) {
-                S = e;
-                r = f;
+        bool joined = false;                                // met the stored trajectory at a checkpoint
+        for (long w0 = s0; w0 < s1; w0 += 64L * seg) {
+#ifdef LDSP_AGC_TRACE
+            n_win++;
+#endif
+            const long a = min(s1, w0 + (long)lane * seg), b = min(s1, a + seg);
+            AgcReg r = T;
+            agc_run_approx(r, p, xl, w0, a);
+            AgcReg S = r;                                   // this segment's start (a guess for lane > 0)
+            agc_run<true>(r, p, xl, a, b, y, status);
+            // lanes whose start is not their left neighbour's exact end: re-run in order
+            // (the shuffles on every lane: a lane reading an inactive one gets garbage)
+            AgcReg pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
+            uint64_t bad = __ballot(lane >= 1 && a < b && !agc_reg_eq(S, pe));
+            while (bad) {
+                const int j = __builtin_ctzll(bad);
+#ifdef LDSP_AGC_TRACE
+                n_rep++;
+#endif
+                const AgcReg e = agc_reg_shfl(r, j - 1);
+                AgcReg f = e;
+                if (lane == 0) agc_run<true>(f, p, xl, w0 + (long)j * seg, min(s1, w0 + (long)j * seg + seg), y, status);
+                f = agc_reg_shfl(f, 0);
+                if (lane == j) {
+                    S = e;
+                    r = f;
+                }
+                pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
+                bad = __ballot(lane > j && a < b && !agc_reg_eq(S, pe));
             }
-            pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
-            bad = __ballot(lane > j && a < b && !agc_reg_eq(S, pe));
+            // the true states at the checkpoints in this window (chunk offsets 64 (q + 1) < cnt)
+            const long o = a - s0;
+            bool match = false;
+            if (cpm && a < s1 && o > 0 && o % kAgcCp == 0) {
+                unsigned* c = cpm + (o / kAgcCp - 1) * 4;
+                match = cp_equal(S, c);
+                if (!match) {
+                    c[0] = __float_as_uint(S.g);
+                    c[1] = __float_as_uint(S.y2p);
+                    c[2] = (unsigned)S.mode;
+                    c[3] = S.timer;
+                }
+            }
+            if (__ballot(match)) {
+                joined = true;
+                break;
+            }
+            T = agc_reg_shfl(r, (int)min(63L, (s1 - 1 - w0) / seg));   // the window's true end state
         }
-        // the true states at the checkpoints inside the chunk (offsets 64 (q + 1) < cnt)
-        if (cp && lane > 0 && (lane * seg) % kAgcCp == 0 && (long)lane * seg < cnt) {
-            unsigned* c = cp + m * (C / kAgcCp) * 4 + ((lane * seg) / kAgcCp - 1) * 4;
-            c[0] = __float_as_uint(S.g);
-            c[1] = __float_as_uint(S.y2p);
-            c[2] = (unsigned)S.mode;
-            c[3] = S.timer;
-        }
-        T = agc_reg_shfl(r, (cnt - 1) / seg);              // the chunk's true end state
-        if (lane == 0) {
+        if (joined) {
+            // the stored end state stands (every lane reads it: T stays wave-uniform)
+            T = AgcReg{__uint_as_float(ldntu(gs + 4)), __uint_as_float(ldntu(gs + 5)), (int)ldntu(gs + 6), ldntu(gs + 7)};
+        } else if (lane == 0) {
             gs[4] = __float_as_uint(T.g);
             gs[5] = __float_as_uint(T.y2p);
             gs[6] = (unsigned)T.mode;
             gs[7] = T.timer;
         }
+#ifdef LDSP_AGC_TRACE
+        n_chunks++;
+#endif
     }
+#ifdef LDSP_AGC_TRACE
+    if (lane == 0)
+        printf("runfix k=%ld chunks=%d windows=%d lane_reruns=%d us=%.1f\n", k, n_chunks, n_win, n_rep,
+               (wall_clock64() - t_start) * 0.01);
+#endif
 }
 
 struct AgcRunfixArgs {
@@ -700,10 +737,11 @@ struct AgcRunfixArgs {
     uint8_t* status;
     unsigned* dbg;
     unsigned* cp;
+    int seg;          // k_agc_runfix_wide: samples per lane per window
 };
 __device__ __forceinline__ void k_agc_runfix_run(const AgcRunfixArgs& a) { k_agc_runfix_body(a.x, a.n, a.st, a.C, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
 LDSP_KERNEL_PAIR(k_agc_runfix, AgcRunfixArgs, k_agc_runfix_run, 64)
-__device__ __forceinline__ void k_agc_runfix_wide_run(const AgcRunfixArgs& a) { k_agc_runfix_wide_body(a.x, a.n, a.st, a.C, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
+__device__ __forceinline__ void k_agc_runfix_wide_run(const AgcRunfixArgs& a) { k_agc_runfix_wide_body(a.x, a.n, a.st, a.C, a.seg, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
 LDSP_KERNEL_PAIR(k_agc_runfix_wide, AgcRunfixArgs, k_agc_runfix_wide_run, 64)
 
 
@@ -879,6 +917,15 @@ static bool agc_runfix_wide(const SpecPlan& p)
     return on && !(p.tsa & 3) && p.C % 64 == 0 && p.C >= 64 && p.C <= 4096;
 }
 
+// samples per lane per window of k_agc_runfix_wide: a window costs ~64 seg
+// approximate + seg exact steps, and the repair stops at the first window
+// whose checkpoints meet the stored trajectory
+static int agc_runfix_seg(const SpecPlan& p)
+{
+    static const int seg = (int)LDSP_KNOB("LDSP_AGC_WSEG", 4);
+    return std::max(1, std::min(seg, p.C / 64));
+}
+
 void agc_spec_front(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
 {
     if (n == 0) return;
@@ -903,7 +950,7 @@ static void agc_rounds(const void* x, size_t n, AgcState* st, const SpecPlan& p,
         if (round == p.rounds) break;
         const AgcRunfixArgs ra{(const float2*)x, (long)n, (const AgcState*)st, p.C, p.nchunks, (unsigned*)p.scratch,
                                (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + round : nullptr,
-                               agc_cp(p)};
+                               agc_cp(p), agc_runfix_seg(p)};
         if (agc_runfix_wide(p))
             launch("k_agc_runfix", k_agc_runfix_wide, k_agc_runfix_wide_many, dim3((unsigned)p.nchunks), dim3(64),
                    (size_t)p.C * sizeof(float2), s, ra);
