@@ -337,6 +337,12 @@ int ldsp_ampmodem_seq_stats(ldsp_ampmodem_t q, uint64_t *batches, uint64_t *redo
  * barrier), written only by the timing variants of a tuning build (zero
  * otherwise).  Synchronises. */
 int ldsp_ampmodem_walk_clocks(ldsp_ampmodem_t q, uint64_t *walk, uint64_t *wait);
+/* Diagnostics, no reference counterpart: the chunk-parallel walker's active time,
+ * cumulative since the object was created -- 10 ns ticks from the moment a walk
+ * has the previous call's state (a walker may be dispatched before that and wait
+ * on the device) to its end, and the number of walks.  Raises LDSP_EHIP if a
+ * walker's wait timed out.  Synchronises. */
+int ldsp_ampmodem_walk_active(ldsp_ampmodem_t q, uint64_t *ticks, uint64_t *count);
 /* Diagnostics, no reference counterpart: the walker's entry margin B = 2^log2_b
  * for the calls that follow (8..21; 0 restores the default).  A narrower
  * margin leaves fewer entries and fails more gap proofs, so more lane-blocks

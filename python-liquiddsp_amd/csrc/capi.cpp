@@ -883,7 +883,20 @@ struct AgcObj {
 };
 
 // ====================================================================== AmpModem
+// Live PLL objects (AmpModem, BroadcastAM): a walker may be launched before its
+// predecessor has finished (amp_pll_stage), holding a CU while it waits; with at
+// most kAmpEarlyMax objects, waiting walkers and the walkers they wait for
+// occupy at most 2 x 64 of the 256 CUs, so every predecessor finds a CU.
+static std::atomic<int> g_amp_live{0};
+static constexpr int kAmpEarlyMax = 64;
+struct AmpLive {
+    AmpLive() { g_amp_live++; }
+    ~AmpLive() { g_amp_live--; }
+    AmpLive(const AmpLive&) = delete;
+    AmpLive& operator=(const AmpLive&) = delete;
+};
 struct AmpObj {
+    AmpLive live;
     float mod_index = 0.75f;
     int type = 0;
     int suppressed = 1;
@@ -900,6 +913,8 @@ struct AmpObj {
     // candidates) can run while call k-1's walker still reads its own slot.
     DevBuf x0[2], mb[2], pll[2], dlh[3];
     unsigned long long ncall = 0;
+    uint32_t wexp = 0;                    // launches issued that write the PLL state (AmpState::wepoch)
+    size_t last_pll_n = 0;                // samples of the last call's PLL launch
     const void* last_stats = nullptr;     // walker counters of the last parallel call (in its scratch slot)
     int cur = 0;
     bool dev_newer = false;
@@ -937,6 +952,7 @@ struct AmpObj {
         upload(ddc, dr, dev);
         upload(dtab, table, dev);
         dst.ensure(sizeof(k::AmpState), dev);
+        st.wepoch = wexp;
         LDSP_HIP(hipMemcpy(dst.p, &st, sizeof(st), hipMemcpyHostToDevice));
         for (int i = 0; i < 2; i++) {
             lph[i].ensure((2 * m) * 8, dev);
@@ -2307,6 +2323,8 @@ static void amp_reset(AmpObj* q)
     if (q->device < 0) return;
     DeviceGuard g(q->device);
     q->sync_all();
+    q->st.wepoch = q->wexp;               // every issued launch has published: the epoch stands
+    q->st.werr = 0;
     LDSP_HIP(hipMemcpy(q->dst.p, &q->st, sizeof(q->st), hipMemcpyHostToDevice));
     for (int i = 0; i < 2; i++) {
         for (DevBuf* b : {&q->lph[i], &q->dch[i]})
@@ -2337,6 +2355,12 @@ int ldsp_ampmodem_get_taps(ldsp_ampmodem_t q, float* lowpass, float* dcblock, fl
         }
     });
 }
+static void amp_check_handoff(const AmpObj* q)
+{
+    if (q->st.werr)
+        throw Error(LDSP_EHIP, "ampmodem: a PLL walker's wait for the previous call's state timed out (1 s); "
+                               "its outputs are not valid");
+}
 int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
 {
     return guard([&] {
@@ -2346,6 +2370,7 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
             q->sync_all();
             LDSP_HIP(hipMemcpy(&q->st, q->dst.p, sizeof(q->st), hipMemcpyDeviceToHost));
             q->dev_newer = false;
+            amp_check_handoff(q);
         }
         if (t) *t = q->st.theta;
         if (d) *d = q->st.dtheta;
@@ -2373,6 +2398,22 @@ int ldsp_ampmodem_walk_stats(ldsp_ampmodem_t q, uint64_t* entries, uint64_t* rep
     });
 }
 
+int ldsp_ampmodem_walk_active(ldsp_ampmodem_t q, uint64_t* ticks, uint64_t* count)
+{
+    return guard([&] {
+        NONNULL(q);
+        k::AmpState st{};
+        if (q->dst.p) {
+            DeviceGuard g(q->device);
+            q->sync_all();
+            LDSP_HIP(hipMemcpy(&st, q->dst.p, sizeof(st), hipMemcpyDeviceToHost));
+            q->st.werr = st.werr;
+            amp_check_handoff(q);
+        }
+        if (ticks) *ticks = st.wact;
+        if (count) *count = st.wact_n;
+    });
+}
 int ldsp_ampmodem_walk_clocks(ldsp_ampmodem_t q, uint64_t* walk, uint64_t* wait)
 {
     return guard([&] {
@@ -2446,6 +2487,7 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     c.alpha_host = q->st.alpha;
     c.y = mbuf;
     c.scratch = k::pll_parallel(n, costas) ? q->pll[sl].ensure(k::pll_scratch_bytes(n), q->device) : nullptr;
+    c.wexp = q->wexp;
     q->last_stats = c.scratch ? (const char*)c.scratch + k::pll_stats_offset(n) : nullptr;
     k::pll_front(c, e.stream);
     const bool par = k::pll_parallel(n, costas);
@@ -2453,8 +2495,22 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     // (A dedicated high-priority walker queue was measured: the ~25 us between
     // walks stayed -- it is the dispatcher waiting for a whole CU to drain for the
     // walker's 135 KiB of LDS, not the cross-queue event -- and the chain slowed.)
-    q->ord.wait(e.stream);
+    // Early hand-off: the carrier walker does not wait for the previous call's
+    // walk on the stream; it is dispatched as soon as its candidates are ready and
+    // waits on the device for the state's epoch (k_pll_walk_body), so the CU it
+    // needs is taken while the previous walk still runs.  The sequential loops and
+    // Costas keep the stream order.
+    static const bool early_on = LDSP_KNOB("LDSP_WALK_EARLY", 1) != 0;
+    // (calls up to 2^26 samples, after one of at most that: the previous walk then
+    // takes < 0.1 s, far inside the walker's 1 s bound on its wait)
+    const bool early = early_on && par && !costas && g_amp_live.load() <= kAmpEarlyMax &&
+                       n <= (size_t(1) << 26) && q->last_pll_n <= (size_t(1) << 26);
+    if (!early) q->ord.wait(e.stream);
     k::pll_back(c, e.stream);
+    if (n > 0) {
+        q->wexp++;
+        q->last_pll_n = n;
+    }
     q->ord.mark(e.stream);                // the true PLL state: the next call's walk may start
     if (!par) q->front.mark(e.stream);
     static const bool dbg_pll = LDSP_KNOB("LDSP_DEBUG_PLL", 0) != 0;

@@ -83,6 +83,14 @@ __device__ __forceinline__ Kick pll_eval(const float* tab, uint32_t i, float2 u0
     return k;
 }
 
+// After a launch's state stores (one thread): release them, then advance the
+// hand-off epoch (AmpState::wepoch) that an early-launched walker waits on.
+__device__ __forceinline__ void amp_publish(AmpState* st, uint32_t next)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(&st->wepoch, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------ sequential
 constexpr int kSeqChunk = 2048;
 
@@ -118,6 +126,7 @@ __device__ __forceinline__ void k_pll_seq_body(PllIn in, long n, AmpState* st, i
         st->dtheta = d;
         st->gth[1 - gcur] = theta;     // exact: the next call's candidates start on the true state
         st->gd[1 - gcur] = d;
+        amp_publish(st, st->wepoch + 1u);
     }
 }
 struct PllSeqArgs {
@@ -259,6 +268,7 @@ __device__ __forceinline__ void k_pll_seqc_body(PllIn in, long n, AmpState* st, 
         st->dtheta = d;
         st->gth[1 - gcur] = theta;     // exact: the next call's candidates start on the true state
         st->gd[1 - gcur] = d;
+        amp_publish(st, st->wepoch + 1u);
     }
 }
 
@@ -1506,9 +1516,10 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
 
 // Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + kRing - 1
 // into the LDS ring meanwhile.
+constexpr unsigned long long kWalkWaitTicks = 100000000ull;   // 1 s of s_memrealtime (100 MHz)
 template <bool F24, bool STATS, int VAR = 0>
 __device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, CandBuf cb,
-                                                           float* __restrict__ y)
+                                                           float* __restrict__ y, uint32_t wexp)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ WalkBufE buf[kRing];      // ring: block c in buf[c % kRing], DMA'd kRing - 1 blocks ahead
@@ -1536,6 +1547,26 @@ __device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    // Hand-off: the launch may be resident before the previous call's walk (or
+    // sequential loop) has stored the true state -- it then holds its CU and has
+    // its first blocks in LDS when the state arrives, instead of waiting for a
+    // whole CU to drain after it.  Wave 0 waits for the state's epoch, bounded:
+    // after 1 s the state is flagged (werr) and the host raises.
+    unsigned long long t_act = 0;
+    if (wave == 0) {
+        const unsigned long long tw = wall_clock64();
+        while (__hip_atomic_load(&st->wepoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != wexp) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - tw > kWalkWaitTicks) {
+                if (lane == 0) st->werr = 1u;
+                break;
+            }
+        }
+        t_act = wall_clock64();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     FullCtx fc;
     fc.x0 = in.x0;
     fc.x = in.x;
@@ -1548,8 +1579,9 @@ __device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, 
     fc.beta = st->beta;
     fc.mod_index = in.mod_index;
     WState g;
-    g.Kb = st->theta - cb.cs[0];         // f(0) = K (chunk 0: A = 0); block 0 has S = 0
-    g.D = st->dtheta - cb.cs[1];
+    // (coherent loads: the state was stored by another launch during this one)
+    g.Kb = __hip_atomic_load(&st->theta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - cb.cs[0];   // f(0) = K
+    g.D = __hip_atomic_load(&st->dtheta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - cb.cs[1];   // (block 0: S = 0)
     g.nrep = 0;
     g.nfb = 0;
     g.nlb = 0;
@@ -1720,6 +1752,9 @@ __device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, 
         const uint32_t pd = cb.pd[L];
         st->theta = cb.ce[2 * L] + g.Kb + (uint32_t)(n - (long)S) * g.D + cb.pth[L] + (uint32_t)n * pd;
         st->dtheta = cb.ce[2 * L + 1] + g.D + pd;
+        st->wact += wall_clock64() - t_act;
+        st->wact_n += 1;
+        amp_publish(st, wexp + 1u);
         cb.stats[0] = g.nrep;
         cb.stats[1] = g.nfb;
         cb.stats[4] = NE;
@@ -1743,15 +1778,16 @@ struct PllWalkArgs {
     AmpState* st;
     CandBuf cb;
     float* y;
+    uint32_t wexp;
 };
 
 template <bool F24, bool STATS, int VAR = 0>
-__global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllWalkArgs a) { k_pll_walk_body<F24, STATS, VAR>(a.in, a.n, a.st, a.cb, a.y); }
+__global__ void __launch_bounds__(kWalkThreads) k_pll_walk(PllWalkArgs a) { k_pll_walk_body<F24, STATS, VAR>(a.in, a.n, a.st, a.cb, a.y, a.wexp); }
 template <bool F24, bool STATS, int VAR = 0>
 __global__ void __launch_bounds__(kWalkThreads) k_pll_walk_many(::ldsp::Many<PllWalkArgs> m)
 {
     const PllWalkArgs& a = m.a[blockIdx.y];
-    k_pll_walk_body<F24, STATS, VAR>(a.in, a.n, a.st, a.cb, a.y);
+    k_pll_walk_body<F24, STATS, VAR>(a.in, a.n, a.st, a.cb, a.y, a.wexp);
 }
 
 
@@ -1931,7 +1967,7 @@ void pll_back(const PllCall& c, hipStream_t s)
         // the walker stores repaired outputs through 32-bit byte offsets from y
         LDSP_REQUIRE(c.n < (size_t(1) << 30), "ampmodem: at most 2^30 samples per call");
         const dim3 g(1), blk(kWalkThreads);
-        const PllWalkArgs a{pll_in(c), (long)c.n, c.st, cand_buf(c), c.y};
+        const PllWalkArgs a{pll_in(c), (long)c.n, c.st, cand_buf(c), c.y, c.wexp};
 #define WALK_LAUNCH(F, S, V) launch("k_pll_walk", k_pll_walk<F, S, V>, k_pll_walk_many<F, S, V>, g, blk, 0, s, a)
         if (c.alpha_host <= 1.0f / 512.0f) {
 #ifdef LDSP_TUNING

@@ -232,6 +232,12 @@ struct AmpState {         // device-resident PLL state
     uint32_t gth[2], gd[2];   // ping-pong guess of the state at the next call's start (candidate end state)
     uint32_t sq_batches;      // k_pll_seqc diagnostics, cumulative: candidate batches stepped,
     uint32_t sq_redone;       //   and batches with a step evaluated by pll_eval (an index left its window)
+    // hand-off: every launch that writes theta / dtheta advances wepoch after them
+    // (release); a walker launched early waits until wepoch equals its call's index
+    uint32_t wepoch;
+    uint32_t werr;            // 1: a walker's hand-off wait timed out (the host raises)
+    unsigned long long wact;  // walker ticks (10 ns) from hand-off to end, cumulative
+    unsigned long long wact_n;
 };
 // One AmpModem / BroadcastAM PLL call.  x0 = lowpass(x) (precomputed), x1 =
 // delay_m(x) via hist (m samples before x[0]); writes Re(v1)/mod (carrier) or
@@ -254,6 +260,7 @@ struct PllCall {
     float alpha_host;
     float* y;
     void* scratch;
+    uint32_t wexp;        // launches that wrote the PLL state before this call's (AmpState::wepoch)
 };
 size_t pll_scratch_bytes(size_t n);
 size_t pll_stats_offset(size_t n);     // 4 x u64 walker counters inside the scratch (debug)

@@ -694,6 +694,12 @@ struct AmpModem {
         check(ldsp_ampmodem_walk_clocks(q, &w, &t));
         return py::make_tuple(w, t);
     }
+    py::tuple walk_active()
+    {
+        uint64_t t, c;
+        check(ldsp_ampmodem_walk_active(q, &t, &c));
+        return py::make_tuple(t, c);
+    }
     py::tuple seq_stats()
     {
         uint64_t b, r;
@@ -1101,6 +1107,7 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("_walk_stats", &AmpModem::walk_stats)
         .def("_taps", &AmpModem::taps)
         .def("_walk_clocks", &AmpModem::walk_clocks)
+        .def("_walk_active", &AmpModem::walk_active)
         .def("_seq_stats", &AmpModem::seq_stats)
         .def("__call__", &AmpModem::demod);
 

@@ -536,6 +536,40 @@ def test_ampmodem_parallel_calls_on_two_streams(ld, ora, rng, carrier):
     assert g.pll_state() == o.pll_state
 
 
+def test_ampmodem_walk_handoff_three_streams(ld, ora, rng):
+    # The carrier walker is dispatched as soon as its candidates are ready and
+    # waits on the device for the previous call's state (AmpState::wepoch,
+    # capi.cpp amp_pll_stage).  Three rotating streams, no host sync between
+    # calls, sequential-loop calls (< 1 024 samples) between walks, and a reset
+    # in the middle (the epoch is re-uploaded): bitwise to the restatement, one
+    # active-time record per walk.
+    import torch
+    x = _am(rng, 200_000, 48000.0, 300.0, amp=1.0)
+    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
+    o = ora.AmpModem(0.5, "dsb", carrier=True)
+    xd = torch.from_numpy(x).cuda()
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    torch.cuda.synchronize()
+    t0, n0 = g._walk_active()
+    assert n0 == 0 and t0 == 0
+    for half, cuts in enumerate(([0, 30_000, 60_000, 61_000, 90_000, 120_000, 120_500],
+                                 [120_500, 150_000, 151_000, 180_000, 200_000])):
+        if half == 1:
+            g.reset()
+            o.reset()
+        outs = []
+        for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+            with torch.cuda.stream(streams[i % 3]):
+                outs.append(g(xd[a:b]))
+        torch.cuda.synchronize()
+        ref = np.concatenate([o(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+        assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), ref)
+        assert g.pll_state() == o.pll_state
+    ticks, walks = g._walk_active()
+    assert walks == 7                  # the calls of >= 1 024 samples
+    assert ticks > 0
+
+
 # ------------------------------------------------------------------ helpers either side of the path
 def test_bytes_to_iq_bitwise(ld, ora, rng):
     import torch
