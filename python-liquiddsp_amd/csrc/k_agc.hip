@@ -127,7 +127,10 @@ __device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, fl
 template <bool SQ, class X>
 __device__ __forceinline__ void agc_run_approx_t(AgcReg& r, const AgcState& p, const X& x, long a, long b)
 {
-    constexpr int kA = 16;
+#ifndef LDSP_AGC_KA
+#define LDSP_AGC_KA 16
+#endif
+    constexpr int kA = LDSP_AGC_KA;
     if (a >= b) return;
     const long full = a + (b - a) / kA * kA;
     float2 nx[kA];
@@ -153,7 +156,10 @@ __device__ __forceinline__ void agc_run_approx(AgcReg& r, const AgcState& p, con
 }
 
 // Run the AGC over x[a, b) (exact).  OUT: write y/status.
-constexpr int kB = 8;
+#ifndef LDSP_AGC_KB
+#define LDSP_AGC_KB 8
+#endif
+constexpr int kB = LDSP_AGC_KB;
 template <bool OUT, bool SQ, class X>
 __device__ __forceinline__ void agc_run_t(AgcReg& r, const AgcState& p, const X& x, long a, long b,
                                           float2* __restrict__ y, uint8_t* __restrict__ status)

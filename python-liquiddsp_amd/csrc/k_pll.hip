@@ -588,12 +588,16 @@ __device__ __forceinline__ uint32_t half_flip(uint32_t dth, int flip)
     return flip ? ((dth + (1u << 30)) >> 31) : 0u;
 }
 
+// 256 threads (4 waves): a 1024-thread workgroup needs 16 free wave slots on one
+// CU, which a full-GPU filter launch on another stream keeps taking -- with 8
+// batched channels the scan waited up to 3 ms for a CU (scripts/batched_timeline.py).
+constexpr int kScanT = 256;
 __device__ __forceinline__ void k_pll_scan_body(CandBuf cb, int flip)
 {
     LDSP_LATENCY_CRITICAL();
-    __shared__ uint32_t sa[1024], sb[1024], sc[1024], sh[1024];
+    __shared__ uint32_t sa[kScanT], sb[kScanT], sc[kScanT], sh[kScanT];
     const int t = threadIdx.x;
-    const long per = (cb.nchc + 1023) / 1024;
+    const long per = (cb.nchc + kScanT - 1) / kScanT;
     const long k0 = min(cb.nchc, (long)t * per), k1 = min(cb.nchc, k0 + per);
     uint32_t a = 0, b = 0, c = 0, h = 0;
     for (long k = k0; k < k1; k++) {
@@ -612,7 +616,7 @@ __device__ __forceinline__ void k_pll_scan_body(CandBuf cb, int flip)
     sc[t] = c;
     sh[t] = h;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {          // inclusive Hillis-Steele
+    for (int off = 1; off < kScanT; off <<= 1) {        // inclusive Hillis-Steele
         const uint32_t pa = t >= off ? sa[t - off] : 0u, pb = t >= off ? sb[t - off] : 0u,
                        pc = t >= off ? sc[t - off] : 0u, ph = t >= off ? sh[t - off] : 0u;
         __syncthreads();
@@ -641,7 +645,7 @@ __device__ __forceinline__ void k_pll_scan_body(CandBuf cb, int flip)
         if ((uint64_t)blk * kBlkE < (uint64_t)ea + m) cb.bbase[blk] = (uint32_t)(k * kCand);
         ea += m;
     }
-    if (t == 1023) *cb.ne = sa[1023];
+    if (t == kScanT - 1) *cb.ne = sa[kScanT - 1];
 }
 
 struct PllScanArgs {
@@ -649,7 +653,7 @@ struct PllScanArgs {
     int flip;
 };
 __device__ __forceinline__ void k_pll_scan_run(const PllScanArgs& a) { k_pll_scan_body(a.cb, a.flip); }
-LDSP_KERNEL_PAIR(k_pll_scan, PllScanArgs, k_pll_scan_run, 1024)
+LDSP_KERNEL_PAIR(k_pll_scan, PllScanArgs, k_pll_scan_run, kScanT)
 
 
 // Entry records, one wave per chunk (4 samples per lane).  Per entry (SoA per
@@ -1941,11 +1945,11 @@ void pll_front(const PllCall& c, hipStream_t s)
                            (approx && !c.costas) ? 1 : 0});
     }
     if (c.costas) {
-        launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(1024), 0, s, PllScanArgs{cb, 1});
+        launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(kScanT), 0, s, PllScanArgs{cb, 1});
         launch("k_pll_reflip", k_pll_reflip, k_pll_reflip_many, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s,
                PllReflipArgs{pll_in(c), (long)c.n, c.st, cb, c.y});
     }
-    launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(1024), 0, s, PllScanArgs{cb, 0});
+    launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(kScanT), 0, s, PllScanArgs{cb, 0});
     launch("k_pll_entries", k_pll_entries, k_pll_entries_many, dim3((unsigned)((cb.nchc + 3) / 4)), dim3(256), 0, s,
            PllEntriesArgs{pll_in(c), (const AmpState*)c.st, cb, (long)c.n});
 }

@@ -20,6 +20,8 @@
 #   ab:<file>:<pkg>,<pkg>..  a script with each package build in turn (LDSP_PKG_DIR), twice
 #   sqab:<pkg>,..  SQ issue counters of k_iir_modal per package build (scripts/iir_sq_ab.sh)
 #   ubench:<b>  a prebuilt microbenchmark scripts/ubench/<b>
+#   p20:<pkg>   bench.py at the driver setting on the package build in <pkg> (A/B builds)
+#   pb:<pkg>    scripts/batched_run.py on the package build in <pkg>
 #   prof        rocprofv3 kernel stats + PMC passes (scripts/prof_round.sh TAG)
 #   py:<file>   python <file> (a one-off script under scripts/)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -79,6 +81,12 @@ for step in "$@"; do
            rc=$?; echo "[$name] rc=$rc"; grep '^{' "$o/$name.log" | cut -c1-330
            grep -o '"single_stream_ms_per_step": [0-9.]*\|"k_pll_cand": {[^}]*}\|"k_agc_chunks": {[^}]*}\|"k_agc_runfix": {[^}]*}\|"k_pll_walk": {[^}]*}\|"repairs": [0-9]*' "$o/$name.log" | tr '\n' ' '; echo
            [ $rc -eq 0 ] || { tail -15 "$o/$name.log"; exit $rc; } ;;
+    p20:*) pk=${step#p20:}; name="p20_$(basename "$pk")"
+           LDSP_PKG_DIR=$pk timeout -k 10 400 $B --steps 20 --warmup 5 > "$o/$name.log" 2>&1
+           rc=$?; echo "[$name] rc=$rc"; grep '^{' "$o/$name.log" | cut -c1-330
+           grep -o '"single_stream_ms_per_step": [0-9.]*\|"k_agc_chunks": {[^}]*}\|"k_agc_runfix": {[^}]*}\|"k_pll_cand": {[^}]*}' "$o/$name.log" | tr '\n' ' '; echo
+           [ $rc -eq 0 ] || { tail -15 "$o/$name.log"; exit $rc; } ;;
+    pb:*) pk=${step#pb:}; LDSP_PKG_DIR=$pk run "pb_$(basename "$pk")" 300 python -u scripts/batched_run.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
