@@ -616,6 +616,75 @@ __device__ __forceinline__ AgcReg agc_reg_shfl(const AgcReg& e, int src)
 {
     return AgcReg{__shfl(e.g, src), __shfl(e.y2p, src), __shfl(e.mode, src), __shfl(e.timer, src)};
 }
+// One chunk m of a repair, from its true start state T, by one wave (the chunk
+// staged in LDS, windows of 64 segments of `seg` samples, the approximate loop to
+// each segment, exact segments, in-order re-runs of segments whose start missed,
+// exit at the first checkpoint that meets the stored trajectory).  Leaves T = the
+// chunk's true end state and records it in gs[4..7] unless the stored one stands.
+__device__ __forceinline__ void agc_chunk_wide(const float2* __restrict__ x, long n, const AgcState& p, int C,
+                                               int seg, long m, unsigned* gs, unsigned* cpm, float2* xs,
+                                               float2* __restrict__ y, uint8_t* __restrict__ status, AgcReg& T)
+{
+    const int lane = threadIdx.x;
+    const long s0 = m * C, s1 = min(n, s0 + C);
+    const int cnt = (int)(s1 - s0);
+    __syncthreads();                                    // the previous chunk's reads of xs are done
+    for (int i = lane; i < cnt; i += 64) xs[i] = x[s0 + i];
+    __syncthreads();
+    const AgcLdsX xl{xs, s0};
+    bool joined = false;                                // met the stored trajectory at a checkpoint
+    for (long w0 = s0; w0 < s1; w0 += 64L * seg) {
+        const long a = min(s1, w0 + (long)lane * seg), b = min(s1, a + seg);
+        AgcReg r = T;
+        agc_run_approx(r, p, xl, w0, a);
+        AgcReg S = r;                                   // this segment's start (a guess for lane > 0)
+        agc_run<true>(r, p, xl, a, b, y, status);
+        // lanes whose start is not their left neighbour's exact end: re-run in order
+        // (the shuffles on every lane: a lane reading an inactive one gets garbage)
+        AgcReg pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
+        uint64_t bad = __ballot(lane >= 1 && a < b && !agc_reg_eq(S, pe));
+        while (bad) {
+            const int j = __builtin_ctzll(bad);
+            const AgcReg e = agc_reg_shfl(r, j - 1);
+            AgcReg f = e;
+            if (lane == 0) agc_run<true>(f, p, xl, w0 + (long)j * seg, min(s1, w0 + (long)j * seg + seg), y, status);
+            f = agc_reg_shfl(f, 0);
+            if (lane == j) {
+                S = e;
+                r = f;
+            }
+            pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
+            bad = __ballot(lane > j && a < b && !agc_reg_eq(S, pe));
+        }
+        // the true states at the checkpoints in this window (chunk offsets 64 (q + 1) < cnt)
+        const long o = a - s0;
+        bool match = false;
+        if (cpm && a < s1 && o > 0 && o % kAgcCp == 0) {
+            unsigned* c = cpm + (o / kAgcCp - 1) * 4;
+            match = cp_equal(S, c);
+            if (!match) {
+                c[0] = __float_as_uint(S.g);
+                c[1] = __float_as_uint(S.y2p);
+                c[2] = (unsigned)S.mode;
+                c[3] = S.timer;
+            }
+        }
+        if (__ballot(match)) {
+            joined = true;
+            break;
+        }
+        T = agc_reg_shfl(r, (int)min(63L, (s1 - 1 - w0) / seg));   // the window's true end state
+    }
+    if (joined) {
+        // the stored end state stands (every lane reads it: T stays wave-uniform)
+        T = AgcReg{__uint_as_float(ldntu(gs + 4)), __uint_as_float(ldntu(gs + 5)), (int)ldntu(gs + 6), ldntu(gs + 7)};
+    } else if (lane == 0) {
+        gs[4] = __float_as_uint(T.g);
+        gs[5] = __float_as_uint(T.y2p);
+        gs[6] = (unsigned)T.mode;
+        gs[7] = T.timer;
+    }
+}
 __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict__ x, long n, const AgcState* st,
                                                         int C, int seg, long nch, unsigned* __restrict__ sc,
                                                         const unsigned long long* __restrict__ flags,
@@ -633,7 +702,7 @@ __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict_
     bool inrun = true;
 #ifdef LDSP_AGC_TRACE
     const long t_start = wall_clock64();
-    int n_chunks = 0, n_rep = 0, n_win = 0;
+    int n_chunks = 0;
 #endif
     for (long m = k; m < nch; m++) {
         unsigned* gs = sc + m * 8;
@@ -647,8 +716,6 @@ __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict_
                     break;                                  // coalesced with the stored trajectory
             }
         }
-        const long s0 = m * C, s1 = min(n, s0 + C);
-        const int cnt = (int)(s1 - s0);
         unsigned* cpm = cp ? cp + m * (C / kAgcCp) * 4 : nullptr;
         if (lane == 0) {
             if (dbg) atomicAdd(dbg, 1u);
@@ -658,76 +725,14 @@ __device__ __forceinline__ void k_agc_runfix_wide_body(const float2* __restrict_
             gs[2] = (unsigned)T.mode;
             gs[3] = T.timer;
         }
-        __syncthreads();                                    // the previous chunk's reads of xs are done
-        for (int i = lane; i < cnt; i += 64) xs[i] = x[s0 + i];
-        __syncthreads();
-        const AgcLdsX xl{xs, s0};
-        bool joined = false;                                // met the stored trajectory at a checkpoint
-        for (long w0 = s0; w0 < s1; w0 += 64L * seg) {
-#ifdef LDSP_AGC_TRACE
-            n_win++;
-#endif
-            const long a = min(s1, w0 + (long)lane * seg), b = min(s1, a + seg);
-            AgcReg r = T;
-            agc_run_approx(r, p, xl, w0, a);
-            AgcReg S = r;                                   // this segment's start (a guess for lane > 0)
-            agc_run<true>(r, p, xl, a, b, y, status);
-            // lanes whose start is not their left neighbour's exact end: re-run in order
-            // (the shuffles on every lane: a lane reading an inactive one gets garbage)
-            AgcReg pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
-            uint64_t bad = __ballot(lane >= 1 && a < b && !agc_reg_eq(S, pe));
-            while (bad) {
-                const int j = __builtin_ctzll(bad);
-#ifdef LDSP_AGC_TRACE
-                n_rep++;
-#endif
-                const AgcReg e = agc_reg_shfl(r, j - 1);
-                AgcReg f = e;
-                if (lane == 0) agc_run<true>(f, p, xl, w0 + (long)j * seg, min(s1, w0 + (long)j * seg + seg), y, status);
-                f = agc_reg_shfl(f, 0);
-                if (lane == j) {
-                    S = e;
-                    r = f;
-                }
-                pe = agc_reg_shfl(r, lane > 0 ? lane - 1 : 0);
-                bad = __ballot(lane > j && a < b && !agc_reg_eq(S, pe));
-            }
-            // the true states at the checkpoints in this window (chunk offsets 64 (q + 1) < cnt)
-            const long o = a - s0;
-            bool match = false;
-            if (cpm && a < s1 && o > 0 && o % kAgcCp == 0) {
-                unsigned* c = cpm + (o / kAgcCp - 1) * 4;
-                match = cp_equal(S, c);
-                if (!match) {
-                    c[0] = __float_as_uint(S.g);
-                    c[1] = __float_as_uint(S.y2p);
-                    c[2] = (unsigned)S.mode;
-                    c[3] = S.timer;
-                }
-            }
-            if (__ballot(match)) {
-                joined = true;
-                break;
-            }
-            T = agc_reg_shfl(r, (int)min(63L, (s1 - 1 - w0) / seg));   // the window's true end state
-        }
-        if (joined) {
-            // the stored end state stands (every lane reads it: T stays wave-uniform)
-            T = AgcReg{__uint_as_float(ldntu(gs + 4)), __uint_as_float(ldntu(gs + 5)), (int)ldntu(gs + 6), ldntu(gs + 7)};
-        } else if (lane == 0) {
-            gs[4] = __float_as_uint(T.g);
-            gs[5] = __float_as_uint(T.y2p);
-            gs[6] = (unsigned)T.mode;
-            gs[7] = T.timer;
-        }
+        agc_chunk_wide(x, n, p, C, seg, m, gs, cpm, xs, y, status, T);
 #ifdef LDSP_AGC_TRACE
         n_chunks++;
 #endif
     }
 #ifdef LDSP_AGC_TRACE
     if (lane == 0)
-        printf("runfix k=%ld chunks=%d windows=%d lane_reruns=%d us=%.1f\n", k, n_chunks, n_win, n_rep,
-               (wall_clock64() - t_start) * 0.01);
+        printf("runfix k=%ld chunks=%d us=%.1f\n", k, n_chunks, (wall_clock64() - t_start) * 0.01);
 #endif
 }
 
@@ -783,10 +788,14 @@ __device__ __forceinline__ void k_agc_flags_run(const AgcFlagsArgs& a) { k_agc_f
 LDSP_KERNEL_PAIR(k_agc_flags, AgcFlagsArgs, k_agc_flags_run, 64)
 
 
+// WIDE: each re-run by the whole wave (agc_chunk_wide, the chunk staged in
+// dynamic LDS) instead of lane 0 alone -- the re-runs are serial, chunk after
+// chunk, so their latency is the verifier's.
+template <bool WIDE>
 __device__ __forceinline__ void k_agc_verify_body(const float2* __restrict__ x, long n, AgcState* st, int C, int W,
                                                    int spec, long nch, unsigned* __restrict__ sc,
                                                    const unsigned long long* __restrict__ flags, float2* __restrict__ y,
-                                                   uint8_t* __restrict__ status, unsigned* dbg, unsigned* cp)
+                                                   uint8_t* __restrict__ status, unsigned* dbg, unsigned* cp, int seg)
 {
     LDSP_LATENCY_CRITICAL();
     const int lane = threadIdx.x;
@@ -824,7 +833,16 @@ __device__ __forceinline__ void k_agc_verify_body(const float2* __restrict__ x, 
             kb = ((wk + L) << 6) + __builtin_ctzll(wd);
             if (kb >= nch) break;
         }
-        if (lane == 0) {
+        if constexpr (WIDE) {
+            extern __shared__ float2 xs[];
+            AgcReg T{__uint_as_float(pred_word(sc, st, kb, 0)), __uint_as_float(pred_word(sc, st, kb, 1)),
+                     (int)pred_word(sc, st, kb, 2), pred_word(sc, st, kb, 3)};
+            agc_chunk_wide(x, n, p, C, seg, kb, sc + kb * 8, cp ? cp + kb * (C / kAgcCp) * 4 : nullptr, xs, y, status, T);
+            if (lane == 0) {
+                if (dbg) dbg[0]++;
+                st->pad[1]++;                               // ldsp_debug_agc_reruns (verifier)
+            }
+        } else if (lane == 0) {
             AgcReg r{__uint_as_float(pred_word(sc, st, kb, 0)), __uint_as_float(pred_word(sc, st, kb, 1)),
                      (int)pred_word(sc, st, kb, 2), pred_word(sc, st, kb, 3)};
             unsigned* en = sc + kb * 8;
@@ -867,9 +885,12 @@ struct AgcVerifyArgs {
     uint8_t* status;
     unsigned* dbg;
     unsigned* cp;
+    int seg;          // k_agc_verify_wide: samples per lane per window
 };
-__device__ __forceinline__ void k_agc_verify_run(const AgcVerifyArgs& a) { k_agc_verify_body(a.x, a.n, a.st, a.C, a.W, a.spec, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp); }
+__device__ __forceinline__ void k_agc_verify_run(const AgcVerifyArgs& a) { k_agc_verify_body<false>(a.x, a.n, a.st, a.C, a.W, a.spec, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp, a.seg); }
 LDSP_KERNEL_PAIR(k_agc_verify, AgcVerifyArgs, k_agc_verify_run, 64)
+__device__ __forceinline__ void k_agc_verify_wide_run(const AgcVerifyArgs& a) { k_agc_verify_body<true>(a.x, a.n, a.st, a.C, a.W, a.spec, a.nch, a.sc, a.flags, a.y, a.status, a.dbg, a.cp, a.seg); }
+LDSP_KERNEL_PAIR(k_agc_verify_wide, AgcVerifyArgs, k_agc_verify_wide_run, 64)
 
 
 __global__ void k_math_eval(int fn, const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y,
@@ -969,10 +990,14 @@ static void agc_verify(const void* x, size_t n, AgcState* st, const SpecPlan& p,
                        hipStream_t s)
 {
     unsigned long long* flags = (unsigned long long*)((unsigned*)p.scratch + agc_flags_offset_words(p.nchunks));
-    launch("k_agc_verify", k_agc_verify, k_agc_verify_many, dim3(1), dim3(64), 0, s,
-           AgcVerifyArgs{(const float2*)x, (long)n, st, p.C, p.W, spec, p.nchunks, (unsigned*)p.scratch,
-                         (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + p.rounds : nullptr,
-                         agc_cp(p)});
+    const AgcVerifyArgs va{(const float2*)x, (long)n, st, p.C, p.W, spec, p.nchunks, (unsigned*)p.scratch,
+                           (const unsigned long long*)flags, (float2*)y, status, p.dbg ? p.dbg + p.rounds : nullptr,
+                           agc_cp(p), agc_runfix_seg(p)};
+    if (agc_runfix_wide(p))
+        launch("k_agc_verify", k_agc_verify_wide, k_agc_verify_wide_many, dim3(1), dim3(64),
+               (size_t)p.C * sizeof(float2), s, va);
+    else
+        launch("k_agc_verify", k_agc_verify, k_agc_verify_many, dim3(1), dim3(64), 0, s, va);
 }
 
 void agc_spec_back(const void* x, size_t n, AgcState* st, const SpecPlan& p, void* y, uint8_t* status, hipStream_t s)
