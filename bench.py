@@ -606,7 +606,11 @@ def components(L, device, reps=5):
     strm = [[torch.cuda.Stream(device) for _ in range(2)] for _ in range(8)]
     out["channels_per_gpu"] = multi_channel(L, device, fused=True, strm=strm)
     out["channels_per_gpu_unfused"] = multi_channel(L, device, strm=strm)
-    bs = [torch.cuda.Stream(device) for _ in range(4)]   # 4 rotating streams: 112.7 GS/s vs 108.8 on 3 (r05h)
+    # 4 rotating streams (112.7 GS/s vs 108.8 on 3, r05h), taken from the 16 above: every
+    # new stream that a process uses takes the next of GPU_MAX_HW_QUEUES (32) hardware
+    # queues, and past 32 streams share queues, i.e. run in order -- new streams here
+    # (after ~27 used) gave 96-100 GS/s against 125-128 in a fresh process (r05zz, r05zw2)
+    bs = [strm[c][0] for c in range(4)]
     out["channels_per_gpu_batched"] = multi_channel_batched(L, device, 8, strm=bs)
     out["channels_per_gpu_batched_16"] = multi_channel_batched(L, device, 16, n=32 << 20, strm=bs)
     return out

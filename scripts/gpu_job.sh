@@ -22,6 +22,7 @@
 #   ubench:<b>  a prebuilt microbenchmark scripts/ubench/<b>
 #   p20:<pkg>   bench.py at the driver setting on the package build in <pkg> (A/B builds)
 #   pb:<pkg>    scripts/batched_run.py on the package build in <pkg>
+#   tb:K=V,...  bench.py at the driver setting with components (no CPU baseline) on the tuning build
 #   prof        rocprofv3 kernel stats + PMC passes (scripts/prof_round.sh TAG)
 #   py:<file>   python <file> (a one-off script under scripts/)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -86,6 +87,10 @@ for step in "$@"; do
            rc=$?; echo "[$name] rc=$rc"; grep '^{' "$o/$name.log" | cut -c1-330
            grep -o '"single_stream_ms_per_step": [0-9.]*\|"k_agc_chunks": {[^}]*}\|"k_agc_runfix": {[^}]*}\|"k_pll_cand": {[^}]*}' "$o/$name.log" | tr '\n' ' '; echo
            [ $rc -eq 0 ] || { tail -15 "$o/$name.log"; exit $rc; } ;;
+    tb:*) kv=${step#tb:}; name="tb_$(echo "$kv" | tr ',=' '_-')"
+          env $(echo "$kv" | tr ',' ' ') LDSP_PKG_DIR=${TB_PKG:-build_tuning} timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$o/$name.log" 2>&1
+          rc=$?; echo "[$name] rc=$rc"; grep -o '"ms_per_step": [0-9.]*\|"channels_per_gpu[a-z_0-9]*": {[^}]*}' "$o/$name.log" | cut -c1-200
+          [ $rc -eq 0 ] || { tail -15 "$o/$name.log"; exit $rc; } ;;
     pb:*) pk=${step#pb:}; LDSP_PKG_DIR=$pk run "pb_$(basename "$pk")" 300 python -u scripts/batched_run.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
