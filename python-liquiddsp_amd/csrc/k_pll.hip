@@ -1799,7 +1799,8 @@ __device__ __forceinline__ void k_delay_hist_body(const float2* __restrict__ x, 
                              long n, int m)
 {
     LDSP_LATENCY_CRITICAL();
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) {
         const long g = n - m + j;
         hist_out[j] = g >= 0 ? x[g] : hist[g + m];
     }
@@ -1812,7 +1813,7 @@ struct DelayHistArgs {
     int m;
 };
 __device__ __forceinline__ void k_delay_hist_run(const DelayHistArgs& a) { k_delay_hist_body(a.x, a.hist, a.hist_out, a.n, a.m); }
-LDSP_KERNEL_PAIR(k_delay_hist, DelayHistArgs, k_delay_hist_run, 256)
+LDSP_KERNEL_PAIR(k_delay_hist, DelayHistArgs, k_delay_hist_run, 64)
 
 
 } // namespace
@@ -1854,7 +1855,10 @@ size_t pll_stats_offset(size_t n) { return pll_layout(n).stats; }
 void delay_hist(const void* x, const void* hist, void* hist_out, size_t n, int m, hipStream_t s)
 {
     if (m <= 0) return;
-    launch("k_delay_hist", k_delay_hist, k_delay_hist_many, dim3(1), dim3(256), 0, s,
+    // one-wave workgroups, one sample per lane: a copy on the chain's critical path
+    // that any free wave slot can take (a 256-thread workgroup waited up to 1.5 ms
+    // behind a full-GPU filter launch with 8 batched channels)
+    launch("k_delay_hist", k_delay_hist, k_delay_hist_many, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s,
            DelayHistArgs{(const float2*)x, (const float2*)hist, (float2*)hist_out, (long)n, m});
     LDSP_HIP(hipGetLastError());
 }
@@ -1931,7 +1935,7 @@ void pll_front(const PllCall& c, hipStream_t s)
 {
     if (c.n == 0) return;
     // delay-line history for the next call (m samples); this call's kernels read the old one
-    launch("k_delay_hist", k_delay_hist, k_delay_hist_many, dim3(1), dim3(64), 0, s,
+    launch("k_delay_hist", k_delay_hist, k_delay_hist_many, dim3((unsigned)((c.m + 63) / 64)), dim3(64), 0, s,
            DelayHistArgs{(const float2*)c.x, (const float2*)c.hist, (float2*)c.hist_out, (long)c.n, c.m});
     if (!pll_parallel(c.n, c.costas)) return;
     const CandBuf cb = cand_buf(c);
