@@ -10,6 +10,6 @@ import bench  # noqa: E402
 import liquiddsp as L  # noqa: E402
 
 dev = torch.device("cuda", 0)
-bs = [torch.cuda.Stream(dev) for _ in range(4)]
+bs = [torch.cuda.Stream(dev) for _ in range(int(os.environ.get("BATCHED_STREAMS", "4")))]
 print(json.dumps({"batched_8": bench.multi_channel_batched(L, dev, 8, strm=bs),
                   "batched_16": bench.multi_channel_batched(L, dev, 16, n=32 << 20, strm=bs)}))
