@@ -570,6 +570,35 @@ def test_ampmodem_walk_handoff_three_streams(ld, ora, rng):
     assert ticks > 0
 
 
+def test_ampmodem_walk_handoff_random_streams(ld, ora, rng):
+    # 48 calls of random sizes (sequential-loop and walker calls mixed, 1 ..
+    # 120 000 samples) on a random one of four streams each, two objects sharing
+    # the streams, no host sync: every hand-off order the epochs allow, bitwise.
+    import torch
+    x = _am(rng, 2_000_000, 48000.0, 300.0, amp=1.0)
+    xd = torch.from_numpy(x).cuda()
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    objs = [(ld.AmpModem(modulation=0.5, type="dsb", carrier=True), ora.AmpModem(0.5, "dsb", carrier=True))
+            for _ in range(2)]
+    sizes = rng.choice([1, 700, 1023, 1024, 5000, 40_000, 120_000], size=48)
+    cuts = [[0], [0]]
+    outs = [[], []]
+    torch.cuda.synchronize()
+    for i, m in enumerate(sizes):
+        j = i % 2
+        a = cuts[j][-1]
+        b = min(len(x), a + int(m))
+        with torch.cuda.stream(streams[int(rng.integers(4))]):
+            outs[j].append(objs[j][0](xd[a:b]))
+        cuts[j].append(b)
+    torch.cuda.synchronize()
+    for j, (g, o) in enumerate(objs):
+        ref = np.concatenate([o(x[a:b]) for a, b in zip(cuts[j][:-1], cuts[j][1:])])
+        assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs[j]]), ref)
+        assert g.pll_state() == o.pll_state
+        assert g._walk_active()[1] == sum(1 for a, b in zip(cuts[j][:-1], cuts[j][1:]) if b - a >= 1024)
+
+
 # ------------------------------------------------------------------ helpers either side of the path
 def test_bytes_to_iq_bitwise(ld, ora, rng):
     import torch
