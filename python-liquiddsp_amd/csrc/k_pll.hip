@@ -600,6 +600,8 @@ __device__ __forceinline__ void k_pll_scan_body(CandBuf cb, int flip)
     const long per = (cb.nchc + kScanT - 1) / kScanT;
     const long k0 = min(cb.nchc, (long)t * per), k1 = min(cb.nchc, k0 + per);
     uint32_t a = 0, b = 0, c = 0, h = 0;
+    // (unrolled: the loads of later chunks issue before the sums of earlier ones)
+#pragma unroll 8
     for (long k = k0; k < k1; k++) {
         a += cb.cnt[k];
         if (k > 0) {
@@ -627,6 +629,7 @@ __device__ __forceinline__ void k_pll_scan_body(CandBuf cb, int flip)
         __syncthreads();
     }
     uint32_t ea = sa[t] - a, eb = sb[t] - b, ec = sc[t] - c, eh = sh[t] ^ h;     // exclusive
+#pragma unroll 8
     for (long k = k0; k < k1; k++) {
         if (k > 0) {
             const uint32_t dd = cb.ce[2 * k - 1] - cb.cs[2 * k + 1];
