@@ -224,6 +224,12 @@ int ldsp_iirfilt_create_tf(const float *b, unsigned int nb, const float *a, unsi
  * path also replaces the speculative exact path of fast-decaying filters;
  * exact mode is unaffected. */
 int ldsp_debug_iir_path(ldsp_iirfilt_t q, int path);
+/* Diagnostics, no reference counterpart: while dev_buf (device memory, at least
+ * objects x 2 x 9 x 4 uint64) is set, every exact SOS launch (k_iir_sect)
+ * writes per (object, component, section wave) the shader clocks spent waiting
+ * for its input / ring space, forming its input tile, in its recursion, and in
+ * all.  NULL turns it off.  Not thread-safe; for timing studies. */
+int ldsp_debug_iir_sect_trace(void *dev_buf);
 int ldsp_debug_iir_modal_info(ldsp_iirfilt_t q, int *ok, int *modes, int *lookback, double *err);
 int ldsp_iirfilt_destroy(ldsp_iirfilt_t q);
 int ldsp_iirfilt_reset(ldsp_iirfilt_t q);
@@ -349,6 +355,13 @@ int ldsp_ampmodem_walk_active(ldsp_ampmodem_t q, uint64_t *ticks, uint64_t *coun
  * are redone sample by sample -- the tests use it to exercise that path.
  * Returns the previous setting. */
 int ldsp_debug_pll_margin(int log2_b);
+/* Test hook, no reference counterpart: the bound of an early-dispatched
+ * walker's wait for the previous call's PLL state (10 ns ticks; 0 restores the
+ * default 1 s), and a skew added to the epoch the object's next walker waits for
+ * (a skew of 1 makes it wait for a launch that never comes, so it times out).
+ * A timed-out walk raises LDSP_EHIP at the object's next call or state read
+ * until ldsp_ampmodem_reset.  Synchronises. */
+int ldsp_debug_ampmodem_handoff(ldsp_ampmodem_t q, uint64_t wait_ticks, int epoch_skew);
 
 /* ------------------------------------------------------------------------
  * Broadcast AM demodulator.  Replaces BroadcastAM (src/demod.hpp:93-153,

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <iterator>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -883,20 +884,84 @@ struct AgcObj {
 };
 
 // ====================================================================== AmpModem
-// Live PLL objects (AmpModem, BroadcastAM): a walker may be launched before its
-// predecessor has finished (amp_pll_stage), holding a CU while it waits; with at
-// most kAmpEarlyMax objects, waiting walkers and the walkers they wait for
-// occupy at most 2 x 64 of the 256 CUs, so every predecessor finds a CU.
-static std::atomic<int> g_amp_live{0};
-static constexpr int kAmpEarlyMax = 64;
+// Live PLL objects (AmpModem, BroadcastAM) per device: a walker may be launched
+// before its predecessor has finished (amp_pll_stage), holding a CU while it
+// waits.  Waiting walkers and the walkers they wait for number at most twice the
+// live objects on the device, so the early path is taken only while those stay
+// within half the device's CUs (amp_early_max: CUs / 4 objects, 64 on MI355X; a
+// CPX-partitioned device gets its own, smaller bound).  Other processes sharing
+// the GPU are not counted: their walkers can only delay a hand-off, which the
+// walker's bounded wait turns into LDSP_EHIP at the next call (amp_check_err),
+// never into a silent result.
+static constexpr int kAmpMaxDev = 64;
+static std::atomic<int> g_amp_live[kAmpMaxDev];
+static int amp_early_max(int dev)
+{
+    static std::atomic<int> cache[kAmpMaxDev];
+    if (dev < 0 || dev >= kAmpMaxDev) return 0;
+    int v = cache[dev].load();
+    if (v == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+        v = cus / 4 > 0 ? cus / 4 : -1;
+        cache[dev] = v;
+    }
+    return v;
+}
 struct AmpLive {
-    AmpLive() { g_amp_live++; }
-    ~AmpLive() { g_amp_live--; }
+    int dev = -1;
+    void set(int d)
+    {
+        if (dev < 0 && d >= 0 && d < kAmpMaxDev) {
+            dev = d;
+            g_amp_live[d]++;
+        }
+    }
+    bool early_ok() const { return dev >= 0 && g_amp_live[dev].load() <= amp_early_max(dev); }
+    AmpLive() = default;
+    ~AmpLive()
+    {
+        if (dev >= 0) g_amp_live[dev]--;
+    }
     AmpLive(const AmpLive&) = delete;
     AmpLive& operator=(const AmpLive&) = delete;
 };
+// Host-mapped error flags (one word per PLL object, taken from page-sized
+// blocks that are never freed: hipHostFree at teardown can outlive the runtime).
+// A walker whose hand-off wait times out sets its object's flag; every call
+// checks it on entry (amp_check_err), so a bad walk is reported at the latest by
+// the object's next call even when no call synchronises in between.
+struct ErrFlags {
+    std::mutex mu;
+    std::vector<uint32_t*> free_list;
+    uint32_t* take()
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (free_list.empty()) {
+            void* p = nullptr;
+            LDSP_HIP(hipHostMalloc(&p, 4096, hipHostMallocMapped | hipHostMallocCoherent));
+            for (int i = 1023; i >= 0; i--) free_list.push_back((uint32_t*)p + i);
+        }
+        uint32_t* f = free_list.back();
+        free_list.pop_back();
+        *(volatile uint32_t*)f = 0;
+        return f;
+    }
+    void give(uint32_t* f)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        free_list.push_back(f);
+    }
+};
+static ErrFlags& err_flags()
+{
+    static ErrFlags* e = new ErrFlags();   // never destroyed (see above)
+    return *e;
+}
+static constexpr unsigned long long kWalkWaitTicks = 100000000ull;   // 1 s of s_memrealtime (100 MHz)
 struct AmpObj {
     AmpLive live;
+    uint32_t* herr = nullptr;             // host-mapped walker timeout flag (ErrFlags)
     float mod_index = 0.75f;
     int type = 0;
     int suppressed = 1;
@@ -953,7 +1018,13 @@ struct AmpObj {
         upload(dtab, table, dev);
         dst.ensure(sizeof(k::AmpState), dev);
         st.wepoch = wexp;
+        if (!herr) herr = err_flags().take();
+        void* hdev = nullptr;
+        LDSP_HIP(hipHostGetDevicePointer(&hdev, herr, 0));
+        st.herr = (uint32_t*)hdev;
+        if (!st.wait_ticks) st.wait_ticks = kWalkWaitTicks;
         LDSP_HIP(hipMemcpy(dst.p, &st, sizeof(st), hipMemcpyHostToDevice));
+        live.set(dev);
         for (int i = 0; i < 2; i++) {
             lph[i].ensure((2 * m) * 8, dev);
             zero_now(lph[i].p, 0, (2 * m) * 8);
@@ -972,6 +1043,13 @@ struct AmpObj {
             }
         }
         device = dev;
+    }
+    AmpObj() = default;
+    AmpObj(const AmpObj&) = delete;
+    AmpObj& operator=(const AmpObj&) = delete;
+    ~AmpObj()
+    {
+        if (herr) err_flags().give(herr);
     }
 };
 
@@ -1106,8 +1184,11 @@ bool enabled() { return g_on.load(std::memory_order_relaxed); }
 // ldsp_profile_only: time only the launches of one kernel (the bench's timed
 // steps record the dominant kernel alone: two events per launch of it instead
 // of two per launch of every kernel)
+// The filter points into an interned, never-freed set of names, so a Scope that
+// compares against it while another thread changes the filter never reads freed
+// memory (the set's nodes do not move).
 std::atomic<const char*> g_only{nullptr};
-std::string g_only_name;
+std::set<std::string>* g_only_names = new std::set<std::string>();
 
 Scope::Scope(hipStream_t s_, const char* n) : s(s_), name(n)
 {
@@ -1147,9 +1228,10 @@ int ldsp_profile_only(const char* kernel)
 {
     return guard([&] {
         std::lock_guard<std::mutex> lk{ldsp::prof::g_mu};
-        ldsp::prof::g_only.store(nullptr);
-        ldsp::prof::g_only_name = kernel ? kernel : "";
-        if (kernel && *kernel) ldsp::prof::g_only.store(ldsp::prof::g_only_name.c_str());
+        if (kernel && *kernel)
+            ldsp::prof::g_only.store(ldsp::prof::g_only_names->insert(kernel).first->c_str());
+        else
+            ldsp::prof::g_only.store(nullptr);
     });
 }
 
@@ -2325,6 +2407,7 @@ static void amp_reset(AmpObj* q)
     q->sync_all();
     q->st.wepoch = q->wexp;               // every issued launch has published: the epoch stands
     q->st.werr = 0;
+    if (q->herr) __atomic_store_n(q->herr, 0u, __ATOMIC_RELEASE);
     LDSP_HIP(hipMemcpy(q->dst.p, &q->st, sizeof(q->st), hipMemcpyHostToDevice));
     for (int i = 0; i < 2; i++) {
         for (DevBuf* b : {&q->lph[i], &q->dch[i]})
@@ -2355,11 +2438,15 @@ int ldsp_ampmodem_get_taps(ldsp_ampmodem_t q, float* lowpass, float* dcblock, fl
         }
     });
 }
-static void amp_check_handoff(const AmpObj* q)
+// A walker whose wait for the previous call's state timed out has walked from a
+// stale state: its call's output is invalid.  Raised at every entry point of the
+// object (and after the host path's synchronisation) until ldsp_ampmodem_reset.
+static void amp_check_err(const AmpObj* q)
 {
-    if (q->st.werr)
-        throw Error(LDSP_EHIP, "ampmodem: a PLL walker's wait for the previous call's state timed out (1 s); "
-                               "its outputs are not valid");
+    const bool dev_flag = q->herr && __atomic_load_n(q->herr, __ATOMIC_ACQUIRE) != 0;
+    if (q->st.werr || dev_flag)
+        throw Error(LDSP_EHIP, "ampmodem: a PLL walker's wait for the previous call's state timed out; "
+                               "the output of that call is not valid (reset the object)");
 }
 int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
 {
@@ -2370,11 +2457,16 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
             q->sync_all();
             LDSP_HIP(hipMemcpy(&q->st, q->dst.p, sizeof(q->st), hipMemcpyDeviceToHost));
             q->dev_newer = false;
-            amp_check_handoff(q);
+            amp_check_err(q);
         }
         if (t) *t = q->st.theta;
         if (d) *d = q->st.dtheta;
     });
+}
+
+int ldsp_debug_iir_sect_trace(void* dev_buf)
+{
+    return k::iir_sect_trace(dev_buf);
 }
 
 int ldsp_debug_pll_margin(int log2_b)
@@ -2408,7 +2500,7 @@ int ldsp_ampmodem_walk_active(ldsp_ampmodem_t q, uint64_t* ticks, uint64_t* coun
             q->sync_all();
             LDSP_HIP(hipMemcpy(&st, q->dst.p, sizeof(st), hipMemcpyDeviceToHost));
             q->st.werr = st.werr;
-            amp_check_handoff(q);
+            amp_check_err(q);
         }
         if (ticks) *ticks = st.wact;
         if (count) *count = st.wact_n;
@@ -2503,7 +2595,7 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     static const bool early_on = LDSP_KNOB("LDSP_WALK_EARLY", 1) != 0;
     // (calls up to 2^26 samples, after one of at most that: the previous walk then
     // takes < 0.1 s, far inside the walker's 1 s bound on its wait)
-    const bool early = early_on && par && !costas && g_amp_live.load() <= kAmpEarlyMax &&
+    const bool early = early_on && par && !costas && q->live.early_ok() &&
                        n <= (size_t(1) << 26) && q->last_pll_n <= (size_t(1) << 26);
     if (!early) q->ord.wait(e.stream);
     k::pll_back(c, e.stream);
@@ -2580,6 +2672,7 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
             }
             return;
         }
+        amp_check_err(q);
         const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
@@ -2603,6 +2696,21 @@ int ldsp_ampmodem_demodulate(ldsp_ampmodem_t q, const void* x, size_t n, void* y
         }
         q->last = e.stream;
         q->stg.finish(e, y, n * 4);
+        if (e.host) amp_check_err(q);         // synchronised: this call's own walk is done
+    });
+}
+
+int ldsp_debug_ampmodem_handoff(ldsp_ampmodem_t q, uint64_t wait_ticks, int epoch_skew)
+{
+    return guard([&] {
+        NONNULL(q);
+        q->ensure_device();
+        DeviceGuard g(q->device);
+        q->sync_all();
+        q->st.wait_ticks = wait_ticks ? (unsigned long long)wait_ticks : kWalkWaitTicks;
+        LDSP_HIP(hipMemcpy((char*)q->dst.p + offsetof(k::AmpState, wait_ticks), &q->st.wait_ticks,
+                           sizeof(q->st.wait_ticks), hipMemcpyHostToDevice));
+        q->wexp += (uint32_t)epoch_skew;
     });
 }
 
@@ -2675,6 +2783,7 @@ int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void* x, size_t n, void* y, 
             }
             return;
         }
+        amp_check_err(q);
         const BufDevice bd(mem, x);
         q->ensure_device();
         DeviceGuard g(q->device);
@@ -2693,6 +2802,7 @@ int ldsp_bcastam_demodulate(ldsp_bcastam_t q, const void* x, size_t n, void* y, 
         }
         q->last = e.stream;
         q->stg.finish(e, y, n * 4);
+        if (e.host) amp_check_err(q);
     });
 }
 
@@ -3040,9 +3150,18 @@ int ldsp_iirfilt_resamp_execute_many(ldsp_iirfilt_t* q, ldsp_resamp_t* rs, const
                                      void* const* y, size_t cap, size_t* nout, int C, void* stream)
 {
     LDSP_RANGE("ldsp_iirfilt_resamp_execute_many");
+    if (q == nullptr || rs == nullptr || C < 1 || C > 4096) {
+        set_last_error("many: 1 .. 4096 objects, filters and resamplers both given");
+        return LDSP_EINVAL;
+    }
+    for (int c = 0; c < C; c++)
+        if (rs[c] == nullptr) {
+            set_last_error("many: NULL resampler");
+            return LDSP_EINVAL;
+        }
     for (int c = 0; c < C; c++)                  // the resamplers must be distinct too
         for (int c2 = 0; c2 < c; c2++)
-            if (rs && rs[c] == rs[c2]) {
+            if (rs[c] == rs[c2]) {
                 set_last_error("many: the objects must be distinct");
                 return LDSP_EINVAL;
             }

@@ -1,0 +1,345 @@
+// k_iir_sect.hip -- exact (float32, bit-identical) SOS cascade for gfx950, one
+// wave per second-order section: the recursion of k_iir_seq (reference
+// src/iirfilter.hpp:292-298 -> iirfilt_crcf_execute_block -> iirfiltsos_execute_df2,
+// oracle/liquid_restate.c sos_df2) with the same operations in the same order.
+//
+// Per section and component the recursion is v0[m] = (u[m] - a1 v0[m-1]) - a2 v0[m-2]
+// (liquid rounds each product: no fma), a chain of three dependent VALU operations
+// per sample (mul -> sub -> sub, ~26 shader clocks measured: scripts/ubench/iir_rec.hip).
+// Everything else is off that chain, so it is taken off the wave that runs it:
+//   * one workgroup per (object, component) -- real taps keep re and im independent;
+//   * wave s < L runs section s's recursion (every lane the same), 4 VALU per sample
+//     (the a2 product is independent), its input read from LDS 16 samples at a
+//     time and its v0 written to an LDS ring 4 at a time;
+//   * the section's input u = y of section s - 1 = (b0 v0 + b1 v0[-1]) + b2 v0[-2]
+//     is formed lane-parallel by wave s from section s - 1's v0 ring, one tile at
+//     a time (8 samples per lane), before the wave walks the tile;
+//   * the I/O wave (wave L) stages input tiles into LDS and forms / stores the last
+//     section's y lane-parallel.
+// Tiles move through rings of 4 tiles with LDS progress counters (LDS operations
+// of a wave are performed in issue order, so a counter written after the data it
+// covers is seen after it); a section runs at most two tiles ahead of its reader,
+// which also reads the last two samples of the previous tile (its y taps).
+#include "batch.hpp"
+#include "kernels.hpp"
+#include "ldsp_common.hpp"
+
+namespace ldsp {
+namespace k {
+
+namespace {
+
+constexpr int kST = 512;                 // samples per tile
+constexpr int kSR = 4;                   // tiles per ring
+constexpr int kRing = kST * kSR;         // floats per ring
+constexpr int kMaxS = kIirPipeMaxSos;
+constexpr int kSectThreads = (kMaxS + 1) * 64;
+
+struct SectArgs {
+    const float* b;       // [3 nsos] (a0-normalised, liquid iirfiltsos layout)
+    const float* a;       // [3 nsos]
+    int nsos;
+    int ncomp;            // 2: complex64 samples, component = blockIdx.x
+    const float* x;
+    long n;
+    float* state;         // [ncomp][3 nsos]: per section v0[-1], v0[-2], v0[-3]
+    float* y;
+    unsigned long long* trace;   // diagnostics (ldsp_debug_iir_sect_trace) or null: per (object, component,
+                                 // wave) shader clocks waiting / forming u / in the recursion, and in all
+};
+
+struct SectShared {
+    float vring[kMaxS][kRing];           // section s's v0, tile k in slot k % kSR
+    float xring[kRing];                  // input component, tile k in slot k % kSR
+    float uscr[kMaxS][kST];              // section s's input tile (s >= 1)
+    int prod[kMaxS];                     // tiles of vring[s] written
+    int cons[kMaxS];                     // tiles of vring[s] read by its reader (wave s + 1, or the I/O wave)
+    int xready, xcons;                   // tiles of xring written (I/O wave) / read (wave 0)
+    int abort;                           // a wait ran past its bound: every later wait returns at once
+};
+
+__device__ __forceinline__ int ctr_load(const int* p)
+{
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// Wait (the whole wave) until *p >= target.  Bounded (2 s; a safety net -- the
+// waits form a chain without cycles, so they always end): past the bound the
+// workgroup is marked aborted and finishes without waiting (its output is then
+// wrong, but the launch always drains).
+constexpr unsigned long long kSectWaitTicks = 200000000ull;    // s_memrealtime, 100 MHz
+__device__ __forceinline__ void ctr_wait(const int* p, int target, int* abort)
+{
+    if (ctr_load(p) >= target) return;
+    const unsigned long long t0 = wall_clock64();
+    while (ctr_load(p) < target && !ctr_load(abort)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > kSectWaitTicks) {
+            __hip_atomic_store(abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+        }
+    }
+    asm volatile("" ::: "memory");
+}
+// Lane 0 publishes v after every LDS access the wave issued before it.
+__device__ __forceinline__ void ctr_publish(int* p, int v, int lane)
+{
+    asm volatile("" ::: "memory");
+    if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+// One sample of the DF-II section (iirfiltsos_execute_df2's v[0] update).
+#define SECT_STEP(u, v)                                   \
+    {                                                     \
+        v = ((u) - a1 * p1) - a2 * p2;                    \
+        p3 = p2;                                          \
+        p2 = p1;                                          \
+        p1 = v;                                           \
+    }
+
+__device__ __forceinline__ void sect_run(const SectArgs& A)
+{
+    __shared__ __attribute__((aligned(16))) SectShared sh;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int L = A.nsos;
+    const int c = blockIdx.x;
+    const long n = A.n;
+    const int ntiles = (int)((n + kST - 1) / kST);
+    float* st = A.state + (long)c * 3 * L;
+    if (tid < kMaxS) {
+        sh.prod[tid] = 0;
+        sh.cons[tid] = 0;
+    }
+    if (tid == 0) {
+        sh.xready = 0;
+        sh.xcons = 0;
+        sh.abort = 0;
+    }
+    float p1 = 0.0f, p2 = 0.0f, p3 = 0.0f;
+    if (wave < L) {
+        p1 = st[3 * wave];
+        p2 = st[3 * wave + 1];
+        p3 = st[3 * wave + 2];
+        // v0 at -1 / -2: the tail the reader of tile 0 takes its y taps from
+        if (lane == 0) {
+            sh.vring[wave][kRing - 1] = p1;
+            sh.vring[wave][kRing - 2] = p2;
+        }
+    }
+    __syncthreads();
+    if (wave < L) {
+        LDSP_LATENCY_CRITICAL();
+        const int s = wave;
+        const float a1 = A.a[3 * s + 1], a2 = A.a[3 * s + 2];
+        float pb0 = 0.0f, pb1 = 0.0f, pb2 = 0.0f;
+        if (s > 0) {
+            pb0 = A.b[3 * (s - 1)];
+            pb1 = A.b[3 * (s - 1) + 1];
+            pb2 = A.b[3 * (s - 1) + 2];
+        }
+        float* const ring = sh.vring[s];
+        const bool tr = A.trace != nullptr;
+        unsigned long long c_wait = 0, c_u = 0, c_loop = 0, c0 = tr ? __builtin_amdgcn_s_memtime() : 0, ca = c0;
+        for (int k = 0; k < ntiles; k++) {
+            const int slot = k & (kSR - 1);
+            const int cnt = (int)min((long)kST, n - (long)k * kST);
+            ctr_wait(s == 0 ? &sh.xready : &sh.prod[s - 1], k + 1, &sh.abort);
+            ctr_wait(&sh.cons[s], k + 2 - kSR, &sh.abort);
+            if (tr) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                c_wait += t - ca;
+                ca = t;
+            }
+            const float* src;
+            if (s == 0) {
+                src = sh.xring + slot * kST;
+            } else {
+                // u = section s - 1's y over the tile, lane-parallel (8 samples per lane)
+                const float* r = sh.vring[s - 1];
+                const int base = slot * kST + 8 * lane;
+                const float2 h = *reinterpret_cast<const float2*>(r + ((base - 2) & (kRing - 1)));
+                const float4 q0 = ld4(r + base), q1 = ld4(r + base + 4);
+                const float e[10] = {h.x, h.y, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+                float u[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) u[i] = (pb0 * e[i + 2] + pb1 * e[i + 1]) + pb2 * e[i];
+                float* us = sh.uscr[s] + 8 * lane;
+                st4(us, make_float4(u[0], u[1], u[2], u[3]));
+                st4(us + 4, make_float4(u[4], u[5], u[6], u[7]));
+                ctr_publish(&sh.cons[s - 1], k + 1, lane);
+                src = sh.uscr[s];
+            }
+            if (tr) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                c_u += t - ca;
+                ca = t;
+            }
+            {
+                // Every lane runs the recursion (the same values from the same LDS
+                // words: reads broadcast, the stores of one address coincide): with
+                // only lane 0 active the LDS accesses of waves on the other SIMDs of
+                // the CU slowed each other's loops 1.5-2.5x (scripts/ubench/iir_lds.hip
+                // M0 / M4: 42-61 against 29 clocks per sample with four waves).
+                // 32 samples per iteration in two register sets (a, b): the reads of
+                // one set are issued before the other set's recursion, so they have
+                // landed when it is needed.  The first iteration is peeled so that
+                // the loop is entered with the LDS operations outstanding in the same
+                // order as around its back edge (the compiler's waits at the loop
+                // head then wait for the reads only, not for the older writes).
+                float* vo = ring + slot * kST;
+                const int c32 = cnt & ~31;
+                auto group = [&](const float4 u0, const float4 u1, const float4 u2, const float4 u3, float* o) {
+                    float4 w0, w1, w2, w3;
+                    SECT_STEP(u0.x, w0.x) SECT_STEP(u0.y, w0.y) SECT_STEP(u0.z, w0.z) SECT_STEP(u0.w, w0.w)
+                    SECT_STEP(u1.x, w1.x) SECT_STEP(u1.y, w1.y) SECT_STEP(u1.z, w1.z) SECT_STEP(u1.w, w1.w)
+                    SECT_STEP(u2.x, w2.x) SECT_STEP(u2.y, w2.y) SECT_STEP(u2.z, w2.z) SECT_STEP(u2.w, w2.w)
+                    SECT_STEP(u3.x, w3.x) SECT_STEP(u3.y, w3.y) SECT_STEP(u3.z, w3.z) SECT_STEP(u3.w, w3.w)
+                    st4(o, w0);
+                    st4(o + 4, w1);
+                    st4(o + 8, w2);
+                    st4(o + 12, w3);
+                };
+                int i = 0;
+                if (c32) {
+                    float4 a0 = ld4(src), a1v = ld4(src + 4), a2v = ld4(src + 8), a3 = ld4(src + 12);
+                    float4 b0 = ld4(src + 16), b1 = ld4(src + 20), b2 = ld4(src + 24), b3 = ld4(src + 28);
+                    __builtin_amdgcn_sched_barrier(0);
+                    for (int pass = 0; pass < 2; pass++) {          // pass 0: the peeled first iteration
+                        const int i1 = pass == 0 ? 32 : c32;
+                        for (; i < i1; i += 32) {
+                            group(a0, a1v, a2v, a3, vo + i);
+                            const int na = (i + 32) & (kST - 1);    // (the tile's start after the last)
+                            a0 = ld4(src + na);
+                            a1v = ld4(src + na + 4);
+                            a2v = ld4(src + na + 8);
+                            a3 = ld4(src + na + 12);
+                            __builtin_amdgcn_sched_barrier(0);
+                            group(b0, b1, b2, b3, vo + i + 16);
+                            const int nb = (i + 48) & (kST - 1);
+                            b0 = ld4(src + nb);
+                            b1 = ld4(src + nb + 4);
+                            b2 = ld4(src + nb + 8);
+                            b3 = ld4(src + nb + 12);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
+                }
+                for (; i < cnt; i++) {
+                    float v;
+                    SECT_STEP(src[i], v)
+                    vo[i] = v;
+                }
+            }
+            if (s == 0) ctr_publish(&sh.xcons, k + 1, lane);
+            ctr_publish(&sh.prod[s], k + 1, lane);
+            if (tr) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                c_loop += t - ca;
+                ca = t;
+            }
+        }
+        if (tr && lane == 0) {
+            unsigned long long* o = A.trace + (((long)blockIdx.y * gridDim.x + blockIdx.x) * (kMaxS + 1) + s) * 4;
+            o[0] = c_wait;
+            o[1] = c_u;
+            o[2] = c_loop;
+            o[3] = __builtin_amdgcn_s_memtime() - c0;
+        }
+        if (lane == 0) {
+            st[3 * s] = p1;
+            st[3 * s + 1] = p2;
+            st[3 * s + 2] = p3;
+        }
+    } else if (wave == L) {
+        // I/O: input tiles into xring, the last section's y out of vring[L - 1]
+        const float lb0 = A.b[3 * (L - 1)], lb1 = A.b[3 * (L - 1) + 1], lb2 = A.b[3 * (L - 1) + 2];
+        const int nc = A.ncomp;
+        const float* r = sh.vring[L - 1];
+        int in_k = 0, out_j = 0;
+        unsigned long long t_idle = 0;
+        while (out_j < ntiles) {
+            bool did = false;
+            const bool ab = ctr_load(&sh.abort) != 0;
+            if (in_k < ntiles && (ab || ctr_load(&sh.xcons) >= in_k + 1 - kSR)) {
+                const long g0 = (long)in_k * kST;
+                float v[kST / 64];
+#pragma unroll
+                for (int i = 0; i < kST / 64; i++) {
+                    const long g = g0 + i * 64 + lane;
+                    v[i] = g < n ? A.x[g * nc + c] : 0.0f;
+                }
+                float* xo = sh.xring + (in_k & (kSR - 1)) * kST;
+#pragma unroll
+                for (int i = 0; i < kST / 64; i++) xo[i * 64 + lane] = v[i];
+                in_k++;
+                ctr_publish(&sh.xready, in_k, lane);
+                did = true;
+            }
+            if (out_j < in_k && (ab || ctr_load(&sh.prod[L - 1]) > out_j)) {
+                asm volatile("" ::: "memory");
+                const long g0 = (long)out_j * kST;
+                const int base = (out_j & (kSR - 1)) * kST;
+#pragma unroll
+                for (int i = 0; i < kST / 64; i++) {
+                    const int m = base + i * 64 + lane;
+                    const float e0 = r[m], e1 = r[(m - 1) & (kRing - 1)], e2 = r[(m - 2) & (kRing - 1)];
+                    const float yv = (lb0 * e0 + lb1 * e1) + lb2 * e2;
+                    const long g = g0 + i * 64 + lane;
+                    if (g < n) A.y[g * nc + c] = yv;
+                }
+                out_j++;
+                ctr_publish(&sh.cons[L - 1], out_j, lane);
+                did = true;
+            }
+            if (!did) {
+                __builtin_amdgcn_s_sleep(1);
+                const unsigned long long t = wall_clock64();
+                if (!t_idle) {
+                    t_idle = t;
+                } else if (t - t_idle > kSectWaitTicks) {
+                    __hip_atomic_store(&sh.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            } else {
+                t_idle = 0;
+            }
+        }
+    }
+}
+
+LDSP_KERNEL_PAIR(k_iir_sect, SectArgs, sect_run, kSectThreads)
+
+unsigned long long* g_sect_trace = nullptr;
+
+} // namespace
+
+int iir_sect_trace(void* dev_buf)
+{
+    g_sect_trace = (unsigned long long*)dev_buf;
+    return 0;
+}
+
+void iir_sect(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s)
+{
+    if (n == 0) return;
+    LDSP_REQUIRE(d.sos && d.nsos >= 1 && d.nsos <= kIirPipeMaxSos, "iir_sect: 1..8 second-order sections");
+    LDSP_REQUIRE(n < (size_t(1) << 40), "iir_sect: call too long");
+    SectArgs a;
+    a.b = d.b;
+    a.a = d.a;
+    a.nsos = d.nsos;
+    a.ncomp = cplx ? 2 : 1;
+    a.x = (const float*)x;
+    a.n = (long)n;
+    a.state = state;
+    a.y = (float*)y;
+    a.trace = g_sect_trace;
+    launch("k_iir_sect", k_iir_sect, k_iir_sect_many, dim3(a.ncomp), dim3((d.nsos + 1) * 64), 0, s, a);
+}
+
+} // namespace k
+} // namespace ldsp

@@ -85,10 +85,12 @@ __device__ __forceinline__ Kick pll_eval(const float* tab, uint32_t i, float2 u0
 
 // After a launch's state stores (one thread): release them, then advance the
 // hand-off epoch (AmpState::wepoch) that an early-launched walker waits on.
+// Monotonic (atomic max): a predecessor that publishes after its successor timed
+// out waiting for it cannot move the epoch backwards.
 __device__ __forceinline__ void amp_publish(AmpState* st, uint32_t next)
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(&st->wepoch, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(&st->wepoch, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ sequential
@@ -1523,7 +1525,6 @@ __device__ __forceinline__ void walk_asm_loop(WalkLoop& w, uint32_t nblk, uint32
 
 // Wave 0 walks the entries of block c; waves 1-7 DMA the entries of block c + kRing - 1
 // into the LDS ring meanwhile.
-constexpr unsigned long long kWalkWaitTicks = 100000000ull;   // 1 s of s_memrealtime (100 MHz)
 template <bool F24, bool STATS, int VAR = 0>
 __device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, CandBuf cb,
                                                            float* __restrict__ y, uint32_t wexp)
@@ -1557,15 +1558,20 @@ __device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, 
     // Hand-off: the launch may be resident before the previous call's walk (or
     // sequential loop) has stored the true state -- it then holds its CU and has
     // its first blocks in LDS when the state arrives, instead of waiting for a
-    // whole CU to drain after it.  Wave 0 waits for the state's epoch, bounded:
-    // after 1 s the state is flagged (werr) and the host raises.
+    // whole CU to drain after it.  Wave 0 waits for the state's epoch, bounded
+    // (AmpState::wait_ticks, 1 s): on a timeout the state is flagged (werr, and the
+    // host-mapped herr that the next call's entry checks) and the host raises.
     unsigned long long t_act = 0;
     if (wave == 0) {
         const unsigned long long tw = wall_clock64();
-        while (__hip_atomic_load(&st->wepoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != wexp) {
+        const unsigned long long wmax = st->wait_ticks;
+        while (__hip_atomic_load(&st->wepoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < wexp) {
             __builtin_amdgcn_s_sleep(2);
-            if (wall_clock64() - tw > kWalkWaitTicks) {
-                if (lane == 0) st->werr = 1u;
+            if (wall_clock64() - tw > wmax) {
+                if (lane == 0) {
+                    st->werr = 1u;
+                    if (st->herr) __hip_atomic_store(st->herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 break;
             }
         }

@@ -82,6 +82,11 @@ void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state,
 // section (k_iir_pipe.hip); iir_seq uses it for SOS cascades of <= kIirPipeMaxSos.
 constexpr int kIirPipeMaxSos = 8;
 void iir_pipe(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
+// The same recursion with one wave per section and one workgroup per (object,
+// component) (k_iir_sect.hip); mergeable in many-calls.  iir_seq uses it for SOS
+// cascades of <= kIirPipeMaxSos sections.
+void iir_sect(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
+int iir_sect_trace(void* dev_buf);     // diagnostics: ldsp_debug_iir_sect_trace
 // Float64 chunked linear scan.  state64: double[2][D] (the DF-II delay line in
 // the layout used by the scan); Apow: double[D*D] matrices: [0] = A^C,
 // [1 + l] = A^{C G 2^l} prepared by the host (see IirScanPlan).
@@ -238,6 +243,9 @@ struct AmpState {         // device-resident PLL state
     uint32_t werr;            // 1: a walker's hand-off wait timed out (the host raises)
     unsigned long long wact;  // walker ticks (10 ns) from hand-off to end, cumulative
     unsigned long long wact_n;
+    unsigned long long wait_ticks;   // bound of the hand-off wait (10 ns ticks; 1 s unless a test shortens it)
+    uint32_t* herr;           // host-mapped flag the walker also sets on a timeout: checked at every call's
+                              // entry, so a timed-out walk is never returned silently (capi.cpp amp_check_err)
 };
 // One AmpModem / BroadcastAM PLL call.  x0 = lowpass(x) (precomputed), x1 =
 // delay_m(x) via hist (m samples before x[0]); writes Re(v1)/mod (carrier) or

@@ -1040,6 +1040,8 @@ PYBIND11_MODULE(_liquiddsp, m)
     });
     // per-kernel device timing (ldsp_profile_*): {kernel: (calls, total_ms)}
     m.def("_debug_pll_margin", [](int lb) { return ldsp_debug_pll_margin(lb); });
+    m.def("_debug_iir_sect_trace", [](uintptr_t p) { check(ldsp_debug_iir_sect_trace((void*)p)); },
+          "diagnostics: device buffer address for k_iir_sect's per-wave clocks (0 = off)");
     m.def("_profile_enable", [](bool on) { check(ldsp_profile_enable(on ? 1 : 0)); });
     m.def("_profile_reset", [] { check(ldsp_profile_reset()); });
     m.def("_profile_only", [](const std::string& k) { check(ldsp_profile_only(k.c_str())); });
@@ -1109,6 +1111,11 @@ PYBIND11_MODULE(_liquiddsp, m)
         .def("_walk_clocks", &AmpModem::walk_clocks)
         .def("_walk_active", &AmpModem::walk_active)
         .def("_seq_stats", &AmpModem::seq_stats)
+        .def("_handoff", [](AmpModem& a, uint64_t wait_ticks, int skew) {
+                 check(ldsp_debug_ampmodem_handoff(a.q, wait_ticks, skew));
+             }, py::arg("wait_ticks"), py::arg("epoch_skew"),
+             "test hook: the early walker's wait bound (10 ns ticks, 0 = 1 s) and a skew of the epoch it waits for "
+             "(ldsp_debug_ampmodem_handoff)")
         .def("__call__", &AmpModem::demod);
 
     // ---- NCO (wrapper.cpp:201-212)
@@ -1197,6 +1204,8 @@ PYBIND11_MODULE(_liquiddsp, m)
                 if (!is_device_tensor(xs[c])) throw py::value_error("execute_many: device tensors only");
                 ins.push_back(dev_in(xs[c], true));
                 if (ins[c].n != ins[0].n) throw py::value_error("execute_many: every input must have the same length");
+                if (!ins[c].device.equal(ins[0].device))
+                    throw py::value_error("execute_many: every input must be on the same device");
             }
             const size_t n = ins[0].n;
             py::object o0 = objs[0];
@@ -1220,7 +1229,7 @@ PYBIND11_MODULE(_liquiddsp, m)
                 }
                 mk(true);
                 check(ldsp_agc_execute_many(q.data(), xp.data(), n, yp.data(), (int)C, ins[0].stream));
-                for (size_t c = 0; c < C; c++) g_state_last = 7;
+                if (n > 0) g_state_last = 7;      // as AGC.__call__
             } else if (py::isinstance<AmpModem>(o0)) {
                 std::vector<ldsp_ampmodem_t> q;
                 for (size_t c = 0; c < C; c++) q.push_back(objs[c].cast<AmpModem&>().q);
@@ -1270,6 +1279,8 @@ PYBIND11_MODULE(_liquiddsp, m)
                 if (!is_device_tensor(xs[c])) throw py::value_error("filter_resample_many: device tensors only");
                 ins.push_back(dev_in(xs[c], c0));
                 if (ins[c].n != ins[0].n) throw py::value_error("filter_resample_many: every input must have the same length");
+                if (!ins[c].device.equal(ins[0].device))
+                    throw py::value_error("filter_resample_many: every input must be on the same device");
                 xp.push_back(ins[c].ptr);
             }
             const size_t n = ins[0].n;

@@ -570,6 +570,38 @@ def test_ampmodem_walk_handoff_three_streams(ld, ora, rng):
     assert ticks > 0
 
 
+def test_ampmodem_walk_timeout_raises(ld, ora, rng):
+    # A walker whose wait for the previous call's state times out has walked
+    # from a stale state.  The object must raise (LDSP_EHIP) at its next call and
+    # state read instead of returning that output silently, the epoch must not go
+    # backwards when the late state arrives, and reset must recover the object
+    # (ldsp_debug_ampmodem_handoff forces the timeout: a 1 ms bound and an epoch
+    # skew of one launch that never comes).
+    import torch
+    x = _am(rng, 160_000, 48000.0, 300.0, amp=1.0)
+    xd = torch.from_numpy(x).cuda()
+    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
+    g(xd[:40_000])
+    torch.cuda.synchronize()
+    g._handoff(100_000, 1)
+    g(xd[40_000:80_000])               # dispatched early, waits for an epoch that never comes
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        g(xd[80_000:120_000])
+    with pytest.raises(RuntimeError, match="timed out"):
+        g.pll_state()
+    with pytest.raises(RuntimeError, match="timed out"):
+        g(x[80_000:120_000])           # host path too
+    g._handoff(0, 0)
+    g.reset()
+    o = ora.AmpModem(0.5, "dsb", carrier=True)
+    outs = [g(xd[a:a + 40_000]) for a in (0, 40_000, 80_000, 120_000)]
+    torch.cuda.synchronize()
+    ref = np.concatenate([o(x[a:a + 40_000]) for a in (0, 40_000, 80_000, 120_000)])
+    assert_bitwise(np.concatenate([t.cpu().numpy() for t in outs]), ref)
+    assert g.pll_state() == o.pll_state
+
+
 def test_ampmodem_walk_handoff_random_streams(ld, ora, rng):
     # 48 calls of random sizes (sequential-loop and walker calls mixed, 1 ..
     # 120 000 samples) on a random one of four streams each, two objects sharing
@@ -782,11 +814,12 @@ def test_device_tensor_path_matches_numpy(ld, ora, rng):
 @pytest.mark.parametrize("cplx", [True, False])
 @pytest.mark.parametrize("order", [1, 2, 5, 8, 16])
 def test_iir_exact_pipeline_call_sizes(ld, ora, rng, cplx, order):
-    """Exact mode of an SOS cascade (k_iir_pipe: one lane per (component,
-    section), skewed two steps per section) across calls of every awkward
-    size: shorter than the skew, odd, one tile (2048 steps) +- 1, several tiles;
-    bit-identical to the sequential restatement and its state carried across."""
-    sizes = [1, 2, 3, 13, 14, 15, 2047, 2048, 2049, 4095, 6000, 3, 40_000]
+    """Exact mode of an SOS cascade (k_iir_sect: a wave per section, one
+    workgroup per component, 512-sample tiles through 4-tile LDS rings) across
+    calls of every awkward size: shorter than a 32-sample group, odd, one tile
+    +- 1, a ring +- 1, several rings; bit-identical to the sequential
+    restatement and its state carried across."""
+    sizes = [1, 2, 3, 13, 14, 15, 31, 32, 33, 511, 512, 513, 2047, 2048, 2049, 4095, 6000, 3, 40_000]
     n = sum(sizes)
     x = cgauss(rng, n) if cplx else np.float32(rng.standard_normal(n))
     cls = ld.ComplexIIRFilter if cplx else ld.RealIIRFilter
@@ -803,7 +836,7 @@ def test_iir_exact_pipeline_call_sizes(ld, ora, rng, cplx, order):
 
 def test_iir_exact_chain_filter_large(ld, ora, rng):
     """The chain's cheby2 order-8 band filter in exact mode on 4 Mi IQ samples in
-    one call (k_iir_pipe), bit-identical to the restatement."""
+    one call (k_iir_sect), bit-identical to the restatement."""
     import torch
     n = 1 << 22
     x = cgauss(rng, n, 0.1)
