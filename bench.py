@@ -132,8 +132,11 @@ def timed_steps(step, steps, warmup, sync, barrier):
 
 
 def reduce_max(elapsed, device):
-    """Max of the per-rank wall times (the job takes as long as its slowest rank)."""
+    """Max of the per-rank wall times (the job takes as long as its slowest rank).
+    gloo reduces host tensors: the value travels on the CPU then."""
     import torch.distributed as tdist
+    if tdist.is_initialized() and tdist.get_backend() == "gloo":
+        device = torch.device("cpu")
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     return float(t.item())
@@ -249,6 +252,58 @@ def cpu_baseline(n_iq, seconds=10.0, c5_seconds=5.0):
     return res
 
 
+def _divergence(y, ref):
+    """|y - ref| / max|ref| over the PCM samples (tests/test_gpu_chain.py)."""
+    d = np.abs(np.asarray(y, np.float64) - np.asarray(ref, np.float64)) / np.max(np.abs(ref))
+    return {"maxrel": float(d.max()), "p999": float(np.quantile(d, 0.999)), "n_diff": int(np.sum(d > 0)),
+            "frac_gt_1e-5": float(np.mean(d > 1e-5))}
+
+
+def parity_check(L, device, n=4 << 20):
+    """The headline chain's measured divergence, next to `value`,
+    outside the timed region and part of the CPU leg (the oracle is the checker
+    here, never the thing measured): on the first n samples of the bench channel
+    (C4, seed 4), the benchmarked fast chain and the exact chain against the CPU
+    restatement (float32, = liquid's arithmetic) and against the restatement with
+    a float64 IIR (the truth the fast IIR approximates).  The gates are those of
+    tests/test_gpu_chain.py: IIR stage <= 1e-6 and <= the float32 recursion's own
+    error; chain p999 / samples off <= the float32 restatement's; largest single
+    deviation <= the spread of liquid's build variants (tests/golden/variants.json)."""
+    from oracle import oracle as O
+    xd = synth_channel(n, 0, device)
+    x = xd.cpu().numpy()
+    fast = AMRadio(L)
+    y_fast = fast(xd).cpu().numpy()
+    ex = AMRadio(L)
+    ex.bandpass.exact = True
+    y_exact = ex(xd).cpu().numpy()
+    iir = L.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2000000)
+    y_iir = iir(xd).cpu().numpy()
+    o = O.IIRFilter(prototype=("cheby2", "lowpass", 1, 8, np.float32(15000 / 2000000), 0.3, 0.7, 60.0))
+    t_iir = o.execute_f64(x)
+    o.reset()
+    f32_iir = o(x)
+
+    def maxrel(a, b):
+        return float(np.max(np.abs(np.asarray(a, np.complex128) - b)) / np.max(np.abs(b)))
+    e_gpu, e_f32 = maxrel(y_iir, t_iir), maxrel(f32_iir, t_iir)
+    truth = O.AMRadio(iir_f64=True)(x)
+    f32 = O.AMRadio()(x)
+    dg, df, dr = _divergence(y_fast, truth), _divergence(f32, truth), _divergence(y_fast, f32)
+    with open(os.path.join(REPO, "tests", "golden", "variants.json")) as f:
+        spread = json.load(f)["chain_variant_spread_maxrel"]
+    exact_bits = bool(y_exact.shape == f32.shape and np.array_equal(y_exact.view(np.uint32), f32.view(np.uint32)))
+    gates = {"iir_stage_le_1e-6": e_gpu <= 1e-6, "iir_stage_le_f32_recursion": e_gpu <= e_f32,
+             "chain_p999_le_f32": dg["p999"] <= df["p999"], "chain_n_diff_le_f32": dg["n_diff"] <= df["n_diff"],
+             "chain_maxrel_le_variant_spread": dg["maxrel"] <= spread, "exact_chain_bitwise": exact_bits}
+    return {"prefix_iq_samples": n, "pcm_samples": int(f32.size),
+            "mode": "fast (default: modal float64 IIR scan; every later stage exact given its input)",
+            "fast_vs_restatement_f32": dr, "fast_vs_f64_iir_truth": dg, "restatement_f32_vs_f64_iir_truth": df,
+            "iir_stage_maxrel_vs_f64": {"gpu_fast": e_gpu, "restatement_f32": e_f32},
+            "variant_spread_maxrel": spread, "exact_mode_bitwise_vs_restatement": exact_bits,
+            "gates": gates, "all_gates_pass": all(gates.values())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -274,21 +329,39 @@ def main():
     ap.add_argument("--scatter", action="store_true",
                     help="rank 0 holds all channels: every step scatters the IQ blocks and gathers the PCM "
                          "(SURVEY 8e) instead of each rank reading a resident channel")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend for world size > 1: nccl (RCCL, one GPU per rank) or gloo, which "
+                         "also runs several ranks on one GPU (rank r on device r mod the device count) -- the "
+                         "multi-process libldsp path on a one-GPU box (tests/test_gpu_dist.py)")
+    ap.add_argument("--walk-early", type=int, choices=(0, 1), default=1,
+                    help="the PLL walker's early hand-off (default on); 0: each walker waits in stream order, so a "
+                         "rocprofv3 kernel trace times the walk itself (the walk-duration cross-check)")
+    ap.add_argument("--dump-pcm", default=None,
+                    help="write each rank's last PCM block to <prefix>.rank<r>.npy (parity checks)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1 or (args.dist and "RANK" in os.environ)
+    if args.backend == "gloo":
+        if args.scatter:
+            ap.error("--scatter sends device tensors: nccl only")
+        local = local % max(1, torch.cuda.device_count())     # (counting devices does not initialise HIP)
     if dist:
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "gloo":
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
     import liquiddsp as L
+    if not args.walk_early:
+        L._debug_walk_early(0)
     x = synth_channel(args.n, rank if args.channel is None else args.channel, device)
     x_all = None
     if args.scatter and dist and rank == 0:
@@ -425,9 +498,11 @@ def main():
                    "pcm_samples_per_step": n_pcm,
                    "carrier_hz": CARRIERS[(rank if args.channel is None else args.channel) % len(CARRIERS)],
                    "seed": 4 if (rank if args.channel is None else args.channel) == 0 else 10 + (rank if args.channel is None else args.channel),
-                   "parallelism": f"channel-per-gpu x{world}" + (" rank0-scatter/gather" if args.scatter and dist else "")},
+                   "parallelism": f"channel-per-gpu x{world}" + (" rank0-scatter/gather" if args.scatter and dist else "")
+                   + (" (gloo, ranks sharing GPUs)" if dist and args.backend == "gloo" else "")},
         "roofline": dict(roofline(dom, dom_ms, achieved, entries, repairs, fallbacks), ms_source=dom_src),
         "streams": nstreams,
+        "walk_early_handoff": bool(args.walk_early),
         "host_ms_per_step": round(host_ms, 4),
         "host_ms_max_step": round(host_max_ms, 4),
         "kernel_events_in_timed_steps": "k_pll_walk only" if kp else False,
@@ -441,6 +516,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:      # the CPU leg runs at N = 1 only
         res["cpu_baseline"] = cpu_baseline(args.n, args.cpu_seconds)
         res["cpu_baseline"]["host"] = host_info()
+        res["parity"] = parity_check(L, device)
+    if args.dump_pcm:
+        np.save(f"{args.dump_pcm}.rank{rank}.npy", y.cpu().numpy())
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist:
@@ -576,6 +654,7 @@ def components(L, device, reps=5):
                             "alg_bytes_fused": 12 * n, "alg_bytes_two_calls": 24 * n}
     del raw
     out["exact_chain_64Mi"] = exact_chain(L, device, n)
+    out["exact_channels_batched_8"] = exact_channels_batched(L, device)
     n = 256 << 20
     xs = torch.complex(torch.randn(n, generator=g, device=device), torch.randn(n, generator=g, device=device))
     nco = L.NCO("nco")
@@ -620,9 +699,10 @@ def exact_chain(L, device, n):
     """The benchmarked chain with bandpass.exact = True -- the configuration whose
     output is bit-identical to the restatement (tests/test_gpu_chain.py) -- one
     64 Mi step on one stream.  Its cheby2 IIR is the float32 DF-II recursion run
-    in order (k_iir_pipe): float32 trajectories of this filter started early from
-    another state do not coalesce bit for bit (scripts/analysis/iir_coalesce.py,
-    DESIGN.md section 4), so no chunk-parallel exact form exists for it."""
+    in order, one wave per section and component (k_iir_sect): float32
+    trajectories of this filter started early from another state do not coalesce
+    bit for bit (scripts/analysis/iir_coalesce.py), so no
+    chunk-parallel exact form exists for it."""
     x = synth_channel(n, 0, device)
     r = AMRadio(L)
     r.bandpass.exact = True
@@ -638,7 +718,36 @@ def exact_chain(L, device, n):
     kern = {k: round(v[1] / v[0], 3) for k, v in L._profile_report().items()}
     del x
     return {"ms_per_step": round(el * 1e3, 2), "Msamples_s": round(n / el / 1e6, 2), "kernels_ms": kern,
-            "iir_kernel": "k_iir_pipe", "note": "exact (bit-identical) mode: the IIR is one sequential recursion"}
+            "iir_kernel": "k_iir_sect", "note": "exact (bit-identical) mode: the IIR is one sequential recursion "
+                                                "per section and component, a wave each"}
+
+
+def exact_channels_batched(L, device, channels=8, n=64 << 20):
+    """C independent exact (bit-identical) AMRadio chains on one GPU, one 64 Mi step
+    each: the exact IIRs of all channels in ONE merged launch (execute_many ->
+    k_iir_sect, one workgroup per channel and component), the resamplers per
+    channel, the AGC / AmpModem / de-emphasis back half batched.  Same bits per
+    channel as its own exact chain (tests/test_gpu_many.py)."""
+    xs = [synth_channel(n, c % 8, device) for c in range(channels)]
+    radios = [AMRadio(L) for _ in range(channels)]
+    for r in radios:
+        r.bandpass.exact = True
+
+    def step(m):
+        ys = L.execute_many([r.bandpass for r in radios], [x[:m] for x in xs])
+        zs = [r.resample(y) for r, y in zip(radios, ys)]
+        a = L.execute_many([r.agc for r in radios], zs)
+        b = L.execute_many([r.am for r in radios], a)
+        return L.execute_many([r.audio_filter for r in radios], b)
+    step(65536)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step(n)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    del xs
+    return {"channels": channels, "iq_samples_per_channel": n, "ms_per_step": round(el * 1e3, 2),
+            "Msamples_s": round(channels * n / el / 1e6, 1), "iir_kernel": "k_iir_sect (merged, one launch)"}
 
 
 def multi_channel_batched(L, device, channels=8, steps=10, n=64 << 20, per=4, strm=None):

@@ -362,6 +362,11 @@ int ldsp_debug_pll_margin(int log2_b);
  * A timed-out walk raises LDSP_EHIP at the object's next call or state read
  * until ldsp_ampmodem_reset.  Synchronises. */
 int ldsp_debug_ampmodem_handoff(ldsp_ampmodem_t q, uint64_t wait_ticks, int epoch_skew);
+/* Diagnostics, no reference counterpart: the walker's early hand-off for the
+ * calls that follow (1 on, the default; 0 off: every walker waits for the
+ * previous walk in stream order, so a kernel trace's k_pll_walk duration is the
+ * walk itself; -1 restores the default).  Returns the previous setting. */
+int ldsp_debug_walk_early(int on);
 
 /* ------------------------------------------------------------------------
  * Broadcast AM demodulator.  Replaces BroadcastAM (src/demod.hpp:93-153,

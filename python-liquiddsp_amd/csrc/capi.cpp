@@ -959,6 +959,8 @@ static ErrFlags& err_flags()
     return *e;
 }
 static constexpr unsigned long long kWalkWaitTicks = 100000000ull;   // 1 s of s_memrealtime (100 MHz)
+// ldsp_debug_walk_early: -1 default (early hand-off on), 0 / 1 forced
+static std::atomic<int> g_walk_early{-1};
 struct AmpObj {
     AmpLive live;
     uint32_t* herr = nullptr;             // host-mapped walker timeout flag (ErrFlags)
@@ -2464,6 +2466,11 @@ int ldsp_ampmodem_get_pll_state(ldsp_ampmodem_t q, uint32_t* t, uint32_t* d)
     });
 }
 
+int ldsp_debug_walk_early(int on)
+{
+    return g_walk_early.exchange(on < 0 ? -1 : (on != 0));
+}
+
 int ldsp_debug_iir_sect_trace(void* dev_buf)
 {
     return k::iir_sect_trace(dev_buf);
@@ -2592,7 +2599,9 @@ static float* amp_pll_stage(AmpObj* q, const Exec& e, const void* dx, size_t n, 
     // waits on the device for the state's epoch (k_pll_walk_body), so the CU it
     // needs is taken while the previous walk still runs.  The sequential loops and
     // Costas keep the stream order.
-    static const bool early_on = LDSP_KNOB("LDSP_WALK_EARLY", 1) != 0;
+    static const bool early_knob = LDSP_KNOB("LDSP_WALK_EARLY", 1) != 0;
+    const int ov = g_walk_early.load(std::memory_order_relaxed);
+    const bool early_on = ov < 0 ? early_knob : ov != 0;
     // (calls up to 2^26 samples, after one of at most that: the previous walk then
     // takes < 0.1 s, far inside the walker's 1 s bound on its wait)
     const bool early = early_on && par && !costas && q->live.early_ok() &&
@@ -3084,7 +3093,7 @@ int ldsp_fmstereo_execute(ldsp_fmstereo_t q, const void* x, size_t n, void* y, s
 // the objects must be distinct.
 // `batchable(c)`: object c's call takes a path whose every kernel has a merged
 // form; otherwise the objects run one after another (the same bits, C times the
-// launches) -- e.g. exact-mode IIR filters, single-sideband AmpModems.
+// launches) -- e.g. exact-mode transfer-function IIR filters, single-sideband AmpModems.
 extern "C++" {
 template <class T, class B, class F>
 static int run_many(T* const* q, int C, void* stream, B&& batchable, F&& one)
@@ -3140,7 +3149,10 @@ int ldsp_iirfilt_execute_many(ldsp_iirfilt_t* q, const void* const* x, size_t n,
     LDSP_RANGE("ldsp_iirfilt_execute_many");
     return run_many(q, C, stream, [&](int c) {
         const IirObj::Path p = q[c]->path_for(n);
-        return p == IirObj::kSpec || p == IirObj::kModal;
+        // exact SOS cascades: k_iir_sect, one workgroup per (object, component)
+        const bool sect = p == IirObj::kSeq && q[c]->sos && q[c]->D > 0 && q[c]->nsos >= 1 &&
+                          q[c]->nsos <= (unsigned)k::kIirPipeMaxSos;
+        return p == IirObj::kSpec || p == IirObj::kModal || sect;
     }, [&](int c) {
         return ldsp_iirfilt_execute(q[c], x[c], n, y[c], LDSP_MEM_DEVICE, stream);
     });

@@ -13,5 +13,5 @@ except ImportError:  # pragma: no cover - numpy-only use
     torch = None
 
 from ._liquiddsp import *  # noqa: F401,F403
-from ._liquiddsp import (__backend__, _debug_pll_margin, _math_eval, _profile_enable, _profile_only,  # noqa: F401
+from ._liquiddsp import (__backend__, _debug_iir_sect_trace, _debug_pll_margin, _debug_walk_early, _math_eval, _profile_enable, _profile_only,  # noqa: F401
                          _profile_report, _profile_reset, device_count)

@@ -1040,6 +1040,8 @@ PYBIND11_MODULE(_liquiddsp, m)
     });
     // per-kernel device timing (ldsp_profile_*): {kernel: (calls, total_ms)}
     m.def("_debug_pll_margin", [](int lb) { return ldsp_debug_pll_margin(lb); });
+    m.def("_debug_walk_early", [](int on) { return ldsp_debug_walk_early(on); },
+          "diagnostics: the PLL walker's early hand-off (1 on, 0 off, -1 default); returns the previous setting");
     m.def("_debug_iir_sect_trace", [](uintptr_t p) { check(ldsp_debug_iir_sect_trace((void*)p)); },
           "diagnostics: device buffer address for k_iir_sect's per-wave clocks (0 = off)");
     m.def("_profile_enable", [](bool on) { check(ldsp_profile_enable(on ? 1 : 0)); });

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(512) k_rec(const float* x, float* out, int rep
     __syncthreads();
     float p1 = 0.f, p2 = 0.f, q1 = 0.f, q2 = 0.f;
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if (V == 1 || V == 3 || V == 9) {
+    if (V == 1 || V == 3 || V == 9 || ((V == 10 || V == 11) && (V == 10 ? lane == 0 : lane < 32))) {
         float u0 = x[lane], u1 = x[lane + 1], u2 = x[lane + 2], u3 = x[lane + 3];
         for (int r = 0; r < reps * (T / 4); r++) {
 #define STEP(u) { const float v = (u - a1 * p1) - a2 * p2; p2 = p1; p1 = v; }
@@ -119,6 +119,9 @@ int main()
         printf("\n");
     };
     run(k_rec<1>, "R1 registers, one chain", 64);
+    run(k_rec<10>, "R10 registers, one chain, exec = lane 0", 64);
+    run(k_rec<11>, "R11 registers, one chain, exec = lanes 0-31", 64);
+    run(k_rec<1>, "R1 again", 64);
     run(k_rec<3>, "R3 registers, two chains interleaved", 64);
     run(k_rec<2>, "R2 LDS in/out, lane 0", 64);
     run(k_rec<4>, "R4 LDS in/out, 4 waves", 256);

@@ -95,6 +95,17 @@ def test_amradio_fast_within_policy(ld, ora):
     dg, df = _divergence(y, truth), _divergence(f32, truth)
     print(f"\nIIR stage: gpu {err_gpu_iir:.3g} restatement-f32 {err_f32_iir:.3g} vs f64; "
           f"chain vs f64-IIR truth: gpu {dg} restatement-f32 {df}")
+    # on record: the figures go to a JSON file as well as the log
+    import json
+    import os
+    rec = os.environ.get("LDSP_PARITY_OUT") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                            "gpurun_out", "parity_fast_chain.json")
+    os.makedirs(os.path.dirname(rec), exist_ok=True)
+    with open(rec, "w") as f:
+        json.dump({"test": "tests/test_gpu_chain.py::test_amradio_fast_within_policy", "prefix_iq_samples": n,
+                   "iir_stage_maxrel_vs_f64": {"gpu_fast": err_gpu_iir, "restatement_f32": err_f32_iir},
+                   "fast_vs_f64_iir_truth": dg, "restatement_f32_vs_f64_iir_truth": df,
+                   "fast_vs_restatement_f32": _divergence(y, f32)}, f, indent=1)
     # Fewer samples off, and less far off in the bulk, than the float32 restatement.
     for k in ("p999", "frac_gt_1e-5", "n_diff"):
         assert dg[k] <= df[k], (k, dg, df)
@@ -103,8 +114,6 @@ def test_amradio_fast_within_policy(ld, ora):
     # trajectories never re-merge): it is random in both, so it is bounded by the
     # spread that liquid-dsp's own build variants show on the same chain
     # (tests/golden/variants.json), not by the restatement's value.
-    import json
-    import os
     meta = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "variants.json")))
     assert dg["maxrel"] <= meta["chain_variant_spread_maxrel"], (dg, meta["chain_variant_spread_maxrel"])
 

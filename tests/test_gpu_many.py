@@ -129,16 +129,58 @@ def test_many_rejects_bad_input(ld):
         ld.execute_many([g], [x.cpu().numpy()])              # host arrays
 
 
-def test_many_unbatchable_paths_fall_back(ld):
-    # exact-mode IIR filters and single-sideband AmpModems take paths without merged
-    # kernels: the many-call runs the objects one after another, same bits
+def test_many_exact_iir_merged_bitwise(ld, ora):
+    # exact-mode SOS cascades (the chain's cheby2 order 8, k_iir_sect: one workgroup
+    # per (object, component)) run as ONE merged launch for all channels: bitwise to
+    # the per-object calls over calls of awkward sizes (state carried across), and
+    # to the restatement on two channels
     import torch
-    C, n = 3, 200_000
-    xs = [torch.from_numpy(_synth(n, c)).cuda() for c in range(C)]
+    C = 8
+    sizes = [100_000, 513, 31, 70_001]
+    n = sum(sizes)
+    xh = [_synth(n, c) for c in range(C)]
+    xs = [torch.from_numpy(x).cuda() for x in xh]
     fa = [ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2e6) for _ in range(C)]
     fb = [ld.ComplexIIRFilter(filter_type="cheby2", order=8, Fc=15000 / 2e6) for _ in range(C)]
     for f in fa + fb:
         f.exact = True
+    got = [[] for _ in range(C)]
+    a = 0
+    for i, m in enumerate(sizes):
+        blk = [x[a:a + m] for x in xs]
+        if i == 1:
+            ld._profile_reset()
+            ld._profile_enable(True)
+        outs = ld.execute_many(fa, blk)
+        if i == 1:
+            torch.cuda.synchronize()
+            ld._profile_enable(False)
+            assert ld._profile_report()["k_iir_sect"][0] == 1, ld._profile_report()
+        for c in range(C):
+            got[c].append(outs[c])
+            ref = fb[c](blk[c])
+            assert torch.equal(outs[c].view(torch.int64), ref.view(torch.int64)), (i, c)
+        a += m
+    for c in (0, C - 1):
+        o = ora.IIRFilter(prototype=("cheby2", "lowpass", 1, 8, np.float32(15000 / 2e6), 0.3, 0.7, 60.0))
+        y = torch.cat(got[c]).cpu().numpy()
+        assert np.array_equal(y.view(np.uint64), o(xh[c]).view(np.uint64)), c
+
+
+def test_many_unbatchable_paths_fall_back(ld):
+    # exact-mode transfer-function IIR filters and single-sideband AmpModems take
+    # paths without merged kernels: the many-call runs the objects one after
+    # another, same bits
+    import torch
+    import scipy.signal as sps
+    C, n = 3, 200_000
+    xs = [torch.from_numpy(_synth(n, c)).cuda() for c in range(C)]
+    b, a = sps.butter(4, 0.002)
+    fa = [ld.CIIRFilter(np.float32(b), np.float32(a)) for _ in range(C)]
+    fb = [ld.CIIRFilter(np.float32(b), np.float32(a)) for _ in range(C)]
+    for f in fa + fb:
+        f.exact = True
+        f._scan_path(1)              # not the speculative chunks: the sequential transfer-function kernel
     got = ld.execute_many(fa, xs)
     for c in range(C):
         assert torch.equal(got[c].view(torch.int64), fb[c](xs[c]).view(torch.int64)), c
@@ -147,3 +189,31 @@ def test_many_unbatchable_paths_fall_back(ld):
     got = ld.execute_many(ma, [x[:20_000] * 5 for x in xs])
     for c in range(C):
         assert torch.equal(got[c].view(torch.int32), mb[c](xs[c][:20_000] * 5).view(torch.int32)), c
+
+
+def test_many_exact_chain_vs_oracle(ld, ora):
+    # the exact (bit-identical) AMRadio chain for several channels at once, as
+    # bench.py's exact_channels_batched steps it: the channels' exact IIRs in one
+    # merged launch, the resamplers per channel, the back half batched -- every
+    # channel bit for bit the restatement's AMRadio on its own input, over two calls
+    import torch
+    C, n = 3, 1 << 20
+    xh = [_synth(2 * n, c) for c in range(C)]
+    xs = [torch.from_numpy(x).cuda() for x in xh]
+    rs = [Radio(ld) for _ in range(C)]
+    for r in rs:
+        r.iir.exact = True
+    outs = [[] for _ in range(C)]
+    for k in range(2):
+        ys = ld.execute_many([r.iir for r in rs], [x[k * n:(k + 1) * n] for x in xs])
+        zs = [r.rs(y) for r, y in zip(rs, ys)]
+        got = ld.execute_many([r.de for r in rs], ld.execute_many([r.am for r in rs],
+                                                                    ld.execute_many([r.agc for r in rs], zs)))
+        for c in range(C):
+            outs[c].append(got[c])
+    torch.cuda.synchronize()
+    for c in range(C):
+        o = ora.AMRadio()
+        ref = np.concatenate([o(xh[c][k * n:(k + 1) * n]) for k in range(2)])
+        y = torch.cat(outs[c]).cpu().numpy()
+        assert y.shape == ref.shape and np.array_equal(y.view(np.uint32), ref.view(np.uint32)), c
