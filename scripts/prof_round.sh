@@ -26,6 +26,12 @@ run fir_write --pmc WRITE_SIZE --output-format csv -d $out/fir_write -o fir -- $
 # the fused front (filter_resample) and its two-call form at 64 Mi (scripts/fused_front.py front)
 R="python3 scripts/fused_front.py front"
 run front_trace --kernel-trace --stats --output-format csv -d $out/front_trace -o front -- $R
+# the walk's duration cross-check: with the early hand-off off every walker waits in
+# stream order, so rocprof's k_pll_walk duration is the walk itself; the same run's
+# JSON line (in the log) carries the walker's own clock (roofline.ms_per_launch)
+run walk0_trace --kernel-trace --stats --output-format csv -d $out/walk0_trace -o walk0 -- $B --walk-early 0
+# the exact SOS cascade (k_iir_sect) and the fast modal IIR at 64 Mi (scripts/iir_exact_time.py)
+run iirx_trace --kernel-trace --stats --output-format csv -d $out/iirx_trace -o iirx -- python3 scripts/iir_exact_time.py
 run front_fetch --pmc FETCH_SIZE --output-format csv -d $out/front_fetch -o front -- $R
 run front_write --pmc WRITE_SIZE --output-format csv -d $out/front_write -o front -- $R
 python3 scripts/pmc_summary.py $out > $out/summary.json && cat $out/summary.json
