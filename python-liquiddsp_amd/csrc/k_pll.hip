@@ -287,16 +287,18 @@ LDSP_KERNEL_PAIR(k_pll_seqc, PllSeqcArgs, k_pll_seqc_run, 256)
 
 // ------------------------------------------------------------------ candidates
 // Candidate chunks of kCand samples.  Per sample the candidate kernel writes
-// its output to y and a record (uint4 = 16 B)
-//   R = (w = theta + 2^21, k1, k2, out)      (the loop's kicks and output at index i = w >> 22)
-// and per chunk its start / end state and its entry count (see the walker).
-// The kicks and output at the neighbouring index i -+ 1 -- what a repair
-// substitutes -- are evaluated by k_pll_entries for the entries only (~1/4 of
-// the samples, in parallel): the candidate's serial loop does one phase-detector
-// evaluation per sample, not three.
+// its output to y and its phase word w = theta + 2^21 (4 B; the table index is
+// w >> 22), and per chunk its start / end state and its entry count (see the
+// walker).  The kicks at the candidate's index and at the neighbouring index
+// i -+ 1 -- what a repair substitutes -- are evaluated by k_pll_entries for the
+// entries only (~1/4 of the samples, in parallel): the candidate's serial loop
+// does one phase-detector evaluation per sample, and stores 8 B per sample (it
+// stored a 16-B record (w, k1, k2, out) until round 6: 67 MB per 1.6 M samples
+// for this kernel and 66 MB for k_pll_entries, which read it back).
 constexpr int kBlkE = 512;        // walker block: entries
 struct CandBuf {
-    uint4* rec;           // [npad] (w, k1, k2, out)
+    uint32_t* rw;         // [npad] candidate phase word w = theta + 2^21 per sample
+    uint32_t* eout;       // [nblkE][kBlkE] candidate output at each entry (the undo of a failed walker block)
     uint32_t* cs;         // [nchc][2] candidate state at chunk start
     uint32_t* ce;         // [nchc][2] candidate state at chunk end
     uint32_t* cnt;        // [nchc] entries per chunk
@@ -331,13 +333,13 @@ constexpr int kB = 8;
 template <bool REC>
 __device__ __forceinline__ void cand_step(const PllIn& in, const float* tab, long s, long a, long b, float2 c0,
                                           float2 c1, float alpha, float beta, uint32_t& theta, uint32_t& d,
-                                          const CandBuf& cb, uint4& rec, float& yo, uint32_t& nent)
+                                          const CandBuf& cb, uint32_t& rec, float& yo, uint32_t& nent)
 {
     const uint32_t ic = tidx(theta);
     const Kick kc = pll_eval(tab, ic, c0, c1, alpha, beta, in.mod_index, in.costas, in.out_idx);
     if (REC) {
         const uint32_t w = theta + (1u << 21);
-        rec = make_uint4(w, kc.k1, kc.k2, __float_as_uint(kc.out));
+        rec = w;
         yo = kc.out;
         nent += (risky(w, cb.B) || s == a || s == b - 1) ? 1u : 0u;
     }
@@ -373,29 +375,29 @@ __device__ __forceinline__ void cand_run(const PllIn& in, const float* tab, long
             n0[j] = in.x0[ii];
             n1[j] = *x1_ptr(in, ii);
         }
-        // REC: the group's records and outputs are kept in registers and stored
-        // back to back after it, so each lane's 128 B of records and 32 B of
-        // outputs reach L2 as whole lines (stored one sample at a time, ~1 us
-        // apart, the partly written lines were evicted by the streaming kernels
-        // beside this one and reached HBM several times over).
-        uint4 r0[kB];
+        // REC: the group's phase words and outputs are kept in registers and
+        // stored back to back after it, so each lane's 32 B of each reach L2 as
+        // whole pieces (stored one sample at a time, ~1 us apart, the partly
+        // written lines were evicted by the streaming kernels beside this one
+        // and reached HBM several times over).
+        uint32_t r0[kB];
         float yo[kB];
 #pragma unroll
         for (int j = 0; j < kB; j++)
             cand_step<REC>(in, tab, i + j, a, b, c0[j], c1[j], alpha, beta, theta, d, cb, r0[j], yo[j], nent);
         if (REC) {
 #pragma unroll
-            for (int j = 0; j < kB; j++) cb.rec[i + j] = r0[j];
+            for (int j = 0; j < kB; j++) cb.rw[i + j] = r0[j];
 #pragma unroll
             for (int j = 0; j < kB; j++) y[i + j] = yo[j];
         }
     }
     for (; i < b; i++) {
-        uint4 r0;
+        uint32_t r0;
         float yo;
         cand_step<REC>(in, tab, i, a, b, in.x0[i], *x1_ptr(in, i), alpha, beta, theta, d, cb, r0, yo, nent);
         if (REC) {
-            cb.rec[i] = r0;
+            cb.rw[i] = r0;
             y[i] = yo;
         }
     }
@@ -684,14 +686,14 @@ __device__ __forceinline__ void k_pll_entries_body(PllIn in, const AmpState* st,
     const float alpha = st->alpha, beta = st->beta;
     const long b0 = k * kCand;
     const int nv = (int)min((long)kCand, n - b0);
-    uint4 R0[4];
+    uint32_t R0[4];
     unsigned long long M[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int i = r * 64 + lane;
         const long sg = b0 + min(i, nv - 1);
-        R0[r] = cb.rec[sg];
-        M[r] = __builtin_amdgcn_ballot_w64(i < nv && (risky(R0[r].x, cb.B) || i == 0 || i == nv - 1));
+        R0[r] = cb.rw[sg];
+        M[r] = __builtin_amdgcn_ballot_w64(i < nv && (risky(R0[r], cb.B) || i == 0 || i == nv - 1));
     }
     const uint32_t pth = cb.pth[k], pd = cb.pd[k];
     uint32_t e = cb.eoff[k];
@@ -709,7 +711,7 @@ __device__ __forceinline__ void k_pll_entries_body(PllIn in, const AmpState* st,
         const long s = b0 + i;
         const uint32_t blk = rank / kBlkE, idx = rank % kBlkE;
         const uint32_t srel = (uint32_t)(s - (long)cb.bbase[blk]);
-        const uint32_t w = R0[r].x, u = w & 0x3fffffu;
+        const uint32_t w = R0[r], u = w & 0x3fffffu;
         const uint32_t A = pth + (uint32_t)s * pd;
         int lo = -(int)u, hi = (1 << 22) - 1 - (int)u;
         if (lne || rne) {
@@ -717,12 +719,17 @@ __device__ __forceinline__ void k_pll_entries_body(PllIn in, const AmpState* st,
             hi = min(hi, B);
         }
         const bool up = u >= (1u << 21);
-        // the loop at the neighbouring table index (one cell up or down) minus the candidate's
+        // the loop at the neighbouring table index (one cell up or down) minus the
+        // candidate's own step (re-evaluated here from the same inputs: the same bits
+        // as k_pll_cand's), whose output is kept for the undo of a failed walker block
         const uint32_t ic = w >> 22;
-        const Kick kn = pll_eval(tab, (up ? ic + 1 : ic - 1) & 0x3ffu, in.x0[s], *x1_ptr(in, s), alpha, beta,
-                                 in.mod_index, in.costas, in.out_idx);
-        const uint32_t dk1 = kn.k1 - R0[r].y, dk2 = kn.k2 - R0[r].z;
+        const float2 ex0 = in.x0[s], ex1 = *x1_ptr(in, s);
+        const Kick kc = pll_eval(tab, ic, ex0, ex1, alpha, beta, in.mod_index, in.costas, in.out_idx);
+        const Kick kn = pll_eval(tab, (up ? ic + 1 : ic - 1) & 0x3ffu, ex0, ex1, alpha, beta, in.mod_index,
+                                 in.costas, in.out_idx);
+        const uint32_t dk1 = kn.k1 - kc.k1, dk2 = kn.k2 - kc.k2;
         const uint32_t out = __float_as_uint(kn.out);
+        cb.eout[(size_t)blk * kBlkE + idx] = __float_as_uint(kc.out);
         // A repair here is right iff f_pre (the offset before it) lies in the
         // intersection of: the presumed one-cell crossing, [-B, B] if the left gap
         // is non-empty, and [-B - dk2, B - dk2] (f_post within B) if the right one
@@ -883,8 +890,8 @@ struct FbKick {
 };
 // walk_fallback's rare full loop step (kept out of line: inlined, its code and
 // registers made every repair of the loop around it ~150 instructions long)
-__device__ __noinline__ FbKick fb_full_step(const float* tab, uint32_t wj, uint32_t cell, uint4 rec, float2 u0v,
-                                            float2 u1v, int j, uint32_t rrel, FullCtx fc)
+__device__ __noinline__ FbKick fb_full_step(const float* tab, uint32_t wj, uint32_t cell, float2 u0v, float2 u1v,
+                                            int j, uint32_t rrel, FullCtx fc)
 {
     const float2 u0 = make_float2(__uint_as_float(rl(__float_as_uint(u0v.x), j)),
                                   __uint_as_float(rl(__float_as_uint(u0v.y), j)));
@@ -892,9 +899,12 @@ __device__ __noinline__ FbKick fb_full_step(const float* tab, uint32_t wj, uint3
                                   __uint_as_float(rl(__float_as_uint(u1v.y), j)));
     const Kick kt = pll_eval(tab, ((wj >> 22) + cell) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas,
                              fc.out_idx);
+    // the candidate's own step at its index (k_pll_cand's bits)
+    const Kick kc = pll_eval(tab, (wj >> 22) & 0x3ffu, u0, u1, fc.alpha, fc.beta, fc.mod_index, fc.costas,
+                             fc.out_idx);
     FbKick r;
-    r.dk1 = rfl(kt.k1 - rl(rec.y, j));
-    r.dk2p = rfl(kt.k2 - rl(rec.z, j)) - rrel * r.dk1;
+    r.dk1 = rfl(kt.k1 - kc.k1);
+    r.dk2p = rfl(kt.k2 - kc.k2) - rrel * r.dk1;
     r.out = rfl(__float_as_uint(kt.out));
     return r;
 }
@@ -911,13 +921,13 @@ __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_
         // samples -- a repair that needs the full loop step reads them lane by lane.
         // (Fully unrolled with guards, not a break: a loop-indexed array would live
         // in scratch memory.)
-        uint4 R[kFbPre];
+        uint32_t R[kFbPre];
         uint32_t A[kFbPre];
         float2 U0[kFbPre], U1[kFbPre];
 #pragma unroll
         for (int q = 0; q < kFbPre; q++) {
             const long s = min(b0 + 64l * q + lane, sb);
-            R[q] = cb.rec[s];
+            R[q] = cb.rw[s];
             const long k = s / kCand;
             A[q] = cb.pth[k] + (uint32_t)s * cb.pd[k];
             U0[q] = fc.x0[s];
@@ -930,14 +940,14 @@ __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_
             if (base <= sb) {
                 const unsigned long long M = __builtin_amdgcn_ballot_w64(base + lane <= sb);
                 const uint32_t srel = (uint32_t)(base + lane - (long)S);
-                uint32_t v = (R[q].x & 0x3fffffu) + g.Kb + srel * g.D + A[q];
+                uint32_t v = (R[q] & 0x3fffffu) + g.Kb + srel * g.D + A[q];
                 unsigned long long mask = __builtin_amdgcn_ballot_w64(v > 0x3fffffu) & M;
                 // the step's repaired outputs: lane j of yv, stored once after the step
                 uint32_t yv = 0;
                 unsigned long long rep = 0;
                 while (mask != 0) {
                     const int j = __builtin_ctzll(mask);
-                    const uint32_t vj = rl(v, j), wj = rl(R[q].x, j);
+                    const uint32_t vj = rl(v, j), wj = rl(R[q], j);
                     const uint32_t rrel = (uint32_t)j + (uint32_t)(base - (long)S);
                     const uint32_t cell = vj >> 22;            // true index - candidate's (mod 1024)
                     const unsigned long long em = __builtin_amdgcn_ballot_w64(esrel == rrel) & emask;
@@ -950,7 +960,7 @@ __device__ __noinline__ WState walk_fallback(WState g, long sa, long sb, uint32_
                     } else {
                         // the loop step at the true index (any number of cells from the
                         // candidate's), evaluated in full; the candidate's kicks from its record
-                        const FbKick fk = fb_full_step(tab, wj, cell, R[q], U0[q], U1[q], j, rrel, fc);
+                        const FbKick fk = fb_full_step(tab, wj, cell, U0[q], U1[q], j, rrel, fc);
                         dk1 = fk.dk1;
                         dk2p = fk.dk2p;
                         out = fk.out;
@@ -1648,12 +1658,11 @@ __device__ __forceinline__ void k_pll_walk_body(PllIn in, long n, AmpState* st, 
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 {
                     // every load first (one round trip), then the stores
-                    const uint32_t* recw = (const uint32_t*)cb.rec;
                     uint32_t sr[kBlkE / 64], cw[kBlkE / 64];
 #pragma unroll
                     for (int q = 0; q < kBlkE / 64; q++) {
                         sr[q] = b.e[0][q * 64 + lane].z;
-                        cw[q] = recw[4 * ((long)S + (q * 64 + lane < cnt ? sr[q] : 0u)) + 3];
+                        cw[q] = cb.eout[(size_t)c * kBlkE + q * 64 + lane];
                     }
 #pragma unroll
                     for (int q = 0; q < kBlkE / 64; q++)
@@ -1827,10 +1836,10 @@ LDSP_KERNEL_PAIR(k_delay_hist, DelayHistArgs, k_delay_hist_run, 64)
 
 } // namespace
 
-// Scratch layout (16-byte aligned pieces): records | cs | ce | cnt | eoff | pth | pd |
-// ne | bbase | entries | stats (256 B).
+// Scratch layout (16-byte aligned pieces): phase words | cs | ce | cnt | eoff | pth | pd |
+// hk | ne | bbase | entries | entry outputs | stats (256 B).
 struct PllLayout {
-    size_t rec, cs, ce, cnt, eoff, pth, pd, hk, ne, bbase, ent, stats, total;
+    size_t rw, cs, ce, cnt, eoff, pth, pd, hk, ne, bbase, ent, eout, stats, total;
     long nchc, nblkE;
 };
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -1841,7 +1850,7 @@ static PllLayout pll_layout(size_t n)
     L.nblkE = (long)((n + kBlkE - 1) / kBlkE);     // entries <= samples
     const size_t nc = (size_t)L.nchc;
     size_t o = 0;
-    L.rec = o;   o = al16(o + nc * kCand * 16);
+    L.rw = o;    o = al16(o + nc * kCand * 4);
     L.cs = o;    o = al16(o + nc * 8);
     L.ce = o;    o = al16(o + nc * 8);
     L.cnt = o;   o = al16(o + nc * 4);
@@ -1852,6 +1861,7 @@ static PllLayout pll_layout(size_t n)
     L.ne = o;    o = al16(o + 4);
     L.bbase = o; o = al16(o + (size_t)L.nblkE * 4);
     L.ent = o;   o = al16(o + (size_t)L.nblkE * 2 * kBlkE * 16);
+    L.eout = o;  o = al16(o + (size_t)L.nblkE * kBlkE * 4);
     L.stats = o; o += 256;
     L.total = o;
     return L;
@@ -1907,7 +1917,8 @@ static CandBuf cand_buf(const PllCall& c)
     const PllLayout L = pll_layout(c.n);
     char* p = (char*)c.scratch;
     CandBuf cb;
-    cb.rec = (uint4*)(p + L.rec);
+    cb.rw = (uint32_t*)(p + L.rw);
+    cb.eout = (uint32_t*)(p + L.eout);
     cb.cs = (uint32_t*)(p + L.cs);
     cb.ce = (uint32_t*)(p + L.ce);
     cb.cnt = (uint32_t*)(p + L.cnt);
