@@ -566,6 +566,25 @@ def _pmc_summary():
 PMC, PMC_SOURCE = _pmc_summary()
 
 
+def rocprof_kernel(run, pattern):
+    """Mean / min / max launch duration of the first kernel whose name contains
+    `pattern` in the latest committed rocprofv3 --stats summary of `run`
+    (profiles/rNN_<run>_kernel_stats.csv, scripts/prof_round.sh): the spread beside
+    the mean (DVFS moves a sustained kernel's clock by ~20 %)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{run}_kernel_stats.csv")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        for r in csv.DictReader(f):
+            if pattern in r["Name"]:
+                return {"calls": int(r["Calls"]), "avg_ms": round(float(r["AverageNs"]) * 1e-6, 4),
+                        "min_ms": round(float(r["MinNs"]) * 1e-6, 4), "max_ms": round(float(r["MaxNs"]) * 1e-6, 4),
+                        "source": os.path.relpath(files[-1], REPO)}
+    return None
+
+
 def pmc_traffic(run, kernel):
     """HBM bytes per launch of `kernel` (a profiling label; the rocprof name may
     carry a variant suffix, e.g. k_fir_fft512x for the k_fir_fft512 label)."""
@@ -617,7 +636,7 @@ def components(L, device, reps=5):
                 "kernel": "k_fir_fft512", "bound": "hbm", "achieved": round(16 * n / ms / 1e6, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(16 * n / ms / 1e6 / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic("fir", "k_fir_fft512"), "traffic_source": PMC_SOURCE,
-                "alg_bytes": 16 * n, "target_frac": 0.5}
+                "alg_bytes": 16 * n, "target_frac": 0.5, "rocprof": rocprof_kernel("fir", "k_fir_fft512x")}
     # BASELINE config 2: ComplexResampler(rate = 48 k / 2 M) on 64 Mi samples, as one
     # call and as the README's 65 536-sample blocks (device tensors, one stream)
     rs = L.ComplexResampler(rate=48000 / 2000000, Fc=48000 / 2000000)
@@ -673,10 +692,14 @@ def components(L, device, reps=5):
     f3 = L.ComplexFIRFilter(kaiser(255, 0.05, 60.0))
     t = timed(lambda: L.mix_down_filter(nco_f, f3, xs))
     (fk, ms), = t.items()
+    rp = rocprof_kernel("fir", "k_fir_fft1024x<true")
+    if rp:
+        for k in ("avg_ms", "min_ms", "max_ms"):
+            rp[k.replace("_ms", "_hbm_frac")] = round(16 * n / rp[k] / 1e6 / HBM_PEAK_GBS, 4)
     out["nco_fir255_256Mi_fused"] = {"kernel": fk, "ms": round(ms, 4), "Msamples_s": round(n / ms / 1e3, 1),
                                      "alg_GBs": round(16 * n / ms / 1e6, 1),
                                      "hbm_frac": round(16 * n / ms / 1e6 / HBM_PEAK_GBS, 4),
-                                     "roof_ms": round(16 * n / HBM_PEAK_GBS / 1e6, 4)}
+                                     "roof_ms": round(16 * n / HBM_PEAK_GBS / 1e6, 4), "rocprof": rp}
     del xs
     out["host_buffers"] = host_path(L, device)
     # both configurations on the same 16 streams: torch hands out streams from a
