@@ -3151,7 +3151,7 @@ int ldsp_iirfilt_execute_many(ldsp_iirfilt_t* q, const void* const* x, size_t n,
         const IirObj::Path p = q[c]->path_for(n);
         // exact SOS cascades: k_iir_sect, one workgroup per (object, component)
         const bool sect = p == IirObj::kSeq && q[c]->sos && q[c]->D > 0 && q[c]->nsos >= 1 &&
-                          q[c]->nsos <= (unsigned)k::kIirPipeMaxSos;
+                          q[c]->nsos <= (unsigned)k::kIirSectMaxSos;
         return p == IirObj::kSpec || p == IirObj::kModal || sect;
     }, [&](int c) {
         return ldsp_iirfilt_execute(q[c], x[c], n, y[c], LDSP_MEM_DEVICE, stream);

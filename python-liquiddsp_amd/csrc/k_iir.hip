@@ -987,12 +987,8 @@ void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state,
 {
     if (n == 0) return;
     LDSP_REQUIRE(d.sos ? d.nsos <= kMaxSos : d.nv <= kMaxTf, "iir: filter order too high for the GPU kernels");
-    if (d.sos && d.nsos >= 1 && d.nsos <= kIirPipeMaxSos) {     // a wave per section (k_iir_sect.hip)
-        static const bool pipe = LDSP_KNOB("LDSP_IIR_PIPE", 0) != 0;
-        if (pipe)
-            iir_pipe(cplx, d, x, n, state, y, s);
-        else
-            iir_sect(cplx, d, x, n, state, y, s);
+    if (d.sos && d.nsos >= 1 && d.nsos <= kIirSectMaxSos) {     // a wave per section (k_iir_sect.hip)
+        iir_sect(cplx, d, x, n, state, y, s);
         return;
     }
     {

@@ -34,7 +34,7 @@ namespace k {
 namespace {
 
 constexpr int kSR = 4;                   // tiles per ring
-constexpr int kMaxS = kIirPipeMaxSos;
+constexpr int kMaxS = kIirSectMaxSos;
 constexpr int kSectThreads = 2 * kMaxS * 64;
 
 struct SectArgs {
@@ -365,7 +365,7 @@ int iir_sect_trace(void* dev_buf)
 void iir_sect(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s)
 {
     if (n == 0) return;
-    LDSP_REQUIRE(d.sos && d.nsos >= 1 && d.nsos <= kIirPipeMaxSos, "iir_sect: 1..8 second-order sections");
+    LDSP_REQUIRE(d.sos && d.nsos >= 1 && d.nsos <= kIirSectMaxSos, "iir_sect: 1..8 second-order sections");
     LDSP_REQUIRE(n < (size_t(1) << 40), "iir_sect: call too long");
     SectArgs a;
     a.b = d.b;

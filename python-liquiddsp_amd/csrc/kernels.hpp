@@ -78,13 +78,11 @@ struct IirDesc {
 // Sequential float32 evaluation (bit-exact with the liquid recursion).
 // state: float[2][3*nsos] (SOS) or float[2][nv] (TF); cplx -> 2 components.
 void iir_seq(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
-// The same recursion with one lane per (component, section), skewed two steps per
-// section (k_iir_pipe.hip); iir_seq uses it for SOS cascades of <= kIirPipeMaxSos.
-constexpr int kIirPipeMaxSos = 8;
-void iir_pipe(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
+// Sections per cascade of the exact kernel below.
+constexpr int kIirSectMaxSos = 8;
 // The same recursion with one wave per section and one workgroup per (object,
 // component) (k_iir_sect.hip); mergeable in many-calls.  iir_seq uses it for SOS
-// cascades of <= kIirPipeMaxSos sections.
+// cascades of <= kIirSectMaxSos sections.
 void iir_sect(bool cplx, const IirDesc& d, const void* x, size_t n, float* state, void* y, hipStream_t s);
 int iir_sect_trace(void* dev_buf);     // diagnostics: ldsp_debug_iir_sect_trace
 // Float64 chunked linear scan.  state64: double[2][D] (the DF-II delay line in

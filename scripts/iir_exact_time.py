@@ -1,5 +1,5 @@
 """Exact-mode IIR timing: the chain's cheby2 order-8 filter (BASELINE C4) with
-bandpass.exact = True on 64 Mi complex samples in one call (k_iir_pipe) and on
+bandpass.exact = True on 64 Mi complex samples in one call (k_iir_sect) and on
 the README's 65 536-sample blocks, next to the fast modal scan."""
 import json
 import os
