@@ -15,9 +15,11 @@
 // keeps a residual), so chunk-parallel speculation cannot be verified by state
 // equality as for the AGC; instead:
 //   k_pll_cand : every chunk of 256 samples runs W samples early from an
-//                extrapolated state and records, per sample, its phase, kicks
+//                extrapolated state and records, per sample, its phase word
 //                and output (the neighbouring index a repair needs is evaluated
-//                later, by k_pll_entries, and only at the entries);
+//                later, by k_pll_entries, and only at the entries); in carrier
+//                mode it also builds the walker's offset model (the chunk scan,
+//                cand_scan_fold), which Costas calls run as k_pll_scan;
 //   k_pll_walk : one workgroup walks 1024-sample blocks in order with the exact offset
 //                of the true trajectory from the candidate; a 64-lane ballot
 //                finds the next sample whose true index differs, only that
@@ -29,6 +31,7 @@
 // short calls); ~2 % of samples need a repair on locked AM signals.
 #include <atomic>
 #include <cstdlib>
+#include <random>
 
 #include "batch.hpp"
 #include "kernels.hpp"
@@ -310,6 +313,8 @@ struct CandBuf {
     uint32_t* bbase;      // [nblkE] S_blk: sample base of walker block c
     uint4* ent;           // [nblkE][2][kBlkE] entry records
     unsigned long long* stats;   // walker counters (LDSP_DEBUG_PLL)
+    unsigned long long* lb;      // [nchc / 64][2][3] the folded scan's look-back granules {value, epoch}
+    uint32_t ep;          // this call's look-back epoch (never 0)
     long nchc;
     int costas;           // Costas phase detector (two stable points half a turn apart)
     uint32_t B;           // risky margin (table-cell units of 2^-22)
@@ -473,15 +478,154 @@ __device__ __forceinline__ void cand_warm_approx(const PllIn& in, long a, long b
 // previous call's walker; the walker carries the exact offset either way.
 // from_true: start from the true state instead of the guess (Costas, whose
 // front waits for the previous walk: chunk 0 is then the true trajectory's branch).
+// The carrier chunk scan (k_pll_scan with flip 0, below) folded into this
+// kernel: one launch fewer per call.  The scan's term for chunk k,
+//     dd_k = ce_d[k-1] - cs_d[k],  c_k = (ce_th[k-1] - k K ce_d[k-1]) - (cs_th[k] - k K cs_d[k])
+// (K = kCand), splits into a part of chunk k - 1's end state and a part of
+// chunk k's start state, so chunk j contributes E_j = (cnt_j, ce_d[j],
+// ce_th[j] - (j + 1) K ce_d[j]) to every LATER chunk's prefix and I_j = (0,
+// -cs_d[j], (j K) cs_d[j] - cs_th[j]) (j > 0) to its own and later ones:
+//     eoff[k] = sum_{j<k} E.cnt,  P_d(k) = sum_{j<k} E.d + sum_{j<=k} I.d,  P_th likewise.
+// A workgroup's 64 chunks (its lanes) thus reduce to one aggregate without its
+// neighbours' states; workgroups chain the aggregates with a decoupled
+// look-back over {value, epoch} granules (the k_iir_modal protocol: a granule
+// counts only when its tag is this call's epoch), the lanes reading 64
+// predecessors at a time.  All additions are mod 2^32, as in k_pll_scan, so
+// the order of the sums does not change a bit.  A predecessor is dispatched
+// before its successor, so the wait ends; it is bounded anyway (wait_ticks,
+// then the state is flagged like a walker's timed-out wait).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)v, d);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v += (uint32_t)__shfl_xor((int)v, d);
+    return v;
+}
+
+__device__ __forceinline__ void cand_scan_fold(AmpState* st, const CandBuf& cb, long k, bool valid, uint32_t nent,
+                                               uint32_t cs_th, uint32_t cs_d, uint32_t ce_th, uint32_t ce_d)
+{
+    const int lane = (int)threadIdx.x;
+    const long b = blockIdx.x;
+    uint32_t e0 = 0, e1 = 0, e2 = 0, i1 = 0, i2 = 0;
+    if (valid) {
+        e0 = nent;
+        e1 = ce_d;
+        e2 = ce_th - (uint32_t)((k + 1) * kCand) * ce_d;
+        if (k > 0) {
+            i1 = 0u - cs_d;
+            i2 = (uint32_t)(k * kCand) * cs_d - cs_th;
+        }
+    }
+    const uint32_t s0 = wave_incl_scan(e0, lane), s1 = wave_incl_scan(e1, lane), s2 = wave_incl_scan(e2, lane);
+    const uint32_t t1 = wave_incl_scan(i1, lane), t2 = wave_incl_scan(i2, lane);
+    const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, 63);
+    const uint32_t g1 = (uint32_t)__builtin_amdgcn_readlane((int)(s1 + t1), 63);
+    const uint32_t g2 = (uint32_t)__builtin_amdgcn_readlane((int)(s2 + t2), 63);
+    const unsigned long long tag = (unsigned long long)cb.ep << 32;
+    unsigned long long* const rec = cb.lb + (size_t)b * 6;      // [0..2] aggregate, [3..5] inclusive prefix
+    if (lane == 0) {
+        __hip_atomic_store(rec + 0, tag | g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rec + 1, tag | g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rec + 2, tag | g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint32_t p0 = 0, p1 = 0, p2 = 0;      // the prefix of every earlier workgroup
+    if (b > 0) {
+        long j0 = b - 1;
+        const unsigned long long tw = wall_clock64(), wmax = st->wait_ticks;
+        for (;;) {
+            // lane i: workgroup j0 - i; both of its records in one round trip, and
+            // only a lane that has neither polls again
+            const long j = j0 - lane;
+            uint32_t v0 = 0, v1 = 0, v2 = 0;
+            int s = j >= 0 ? 0 : 3;                      // before chunk 0: an inclusive zero
+            for (;;) {
+                if (s == 0) {
+                    const unsigned long long* r = cb.lb + (size_t)j * 6;
+                    unsigned long long q[6];
+#pragma unroll
+                    for (int e = 0; e < 6; e++) q[e] = __hip_atomic_load(r + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((q[3] >> 32) == cb.ep && (q[4] >> 32) == cb.ep && (q[5] >> 32) == cb.ep) {
+                        s = 2;
+                        v0 = (uint32_t)q[3], v1 = (uint32_t)q[4], v2 = (uint32_t)q[5];
+                    } else if ((q[0] >> 32) == cb.ep && (q[1] >> 32) == cb.ep && (q[2] >> 32) == cb.ep) {
+                        s = 1;
+                        v0 = (uint32_t)q[0], v1 = (uint32_t)q[1], v2 = (uint32_t)q[2];
+                    }
+                }
+                const unsigned long long inc = __builtin_amdgcn_ballot_w64(s >= 2);
+                const int f = inc ? __builtin_ctzll(inc) : 64;
+                const unsigned long long need = f == 64 ? ~0ull : ((1ull << f) - 1ull);
+                if (!(__builtin_amdgcn_ballot_w64(s == 0) & need)) break;
+                if (wall_clock64() - tw > wmax) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+            const unsigned long long inc = __builtin_amdgcn_ballot_w64(s >= 2);
+            const int f = inc ? __builtin_ctzll(inc) : 64;
+            if (__builtin_amdgcn_ballot_w64(s == 0) & (f == 64 ? ~0ull : ((1ull << f) - 1ull))) {   // timed out
+                if (lane == 0) {
+                    st->werr = 1u;
+                    if (st->herr) __hip_atomic_store(st->herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                break;
+            }
+            const bool take = lane <= f;                 // aggregates before the first inclusive prefix, and it
+            p0 += wave_sum_u32(take ? v0 : 0u);
+            p1 += wave_sum_u32(take ? v1 : 0u);
+            p2 += wave_sum_u32(take ? v2 : 0u);
+            if (f < 64) break;
+            j0 -= 64;
+        }
+    }
+    if (lane == 0) {
+        __hip_atomic_store(rec + 3, tag | (p0 + g0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rec + 4, tag | (p1 + g1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rec + 5, tag | (p2 + g2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!valid) return;
+    const uint32_t ea = p0 + s0 - e0;
+    cb.eoff[k] = ea;
+    cb.pd[k] = p1 + (s1 - e1) + t1;
+    cb.pth[k] = p2 + (s2 - e2) + t2;
+    const uint32_t blk = (ea + kBlkE - 1) / kBlkE;     // first walker block starting at or after ea
+    if ((uint64_t)blk * kBlkE < (uint64_t)ea + nent) cb.bbase[blk] = (uint32_t)(k * kCand);
+    if (k == cb.nchc - 1) *cb.ne = ea + nent;
+}
+
+__device__ __forceinline__ void cand_chunk(PllIn in, long n, AmpState* st, int gcur, CandBuf cb, float* __restrict__ y,
+                                           int warm, int from_true, int approx, const float* tab, long k,
+                                           uint32_t& nent, uint32_t& cs_th, uint32_t& cs_d, uint32_t& ce_th,
+                                           uint32_t& ce_d);
+
 __device__ __forceinline__ void k_pll_cand_body(PllIn in, long n, AmpState* st, int gcur, CandBuf cb,
-                                                 float* __restrict__ y, int warm, int from_true, int approx)
+                                                 float* __restrict__ y, int warm, int from_true, int approx, int fold)
 {
     LDSP_LATENCY_CRITICAL();
     __shared__ float tab[1024];
     for (int i = threadIdx.x; i < 1024; i += 64) tab[i] = in.table[i];
     __syncthreads();
     const long k = (long)blockIdx.x * 64 + threadIdx.x;
-    if (k >= cb.nchc) return;
+    const bool valid = k < cb.nchc;
+    uint32_t nent = 0, cs_th = 0, cs_d = 0, ce_th = 0, ce_d = 0;
+    if (valid) cand_chunk(in, n, st, gcur, cb, y, warm, from_true, approx, tab, k, nent, cs_th, cs_d, ce_th, ce_d);
+    if (fold) cand_scan_fold(st, cb, k, valid, nent, cs_th, cs_d, ce_th, ce_d);   // the whole wave, converged
+}
+
+// Chunk k's candidate (k_pll_cand_body): start / end state and entry count.
+__device__ __forceinline__ void cand_chunk(PllIn in, long n, AmpState* st, int gcur, CandBuf cb, float* __restrict__ y,
+                                           int warm, int from_true, int approx, const float* tab, long k,
+                                           uint32_t& nent, uint32_t& cs_th, uint32_t& cs_d, uint32_t& ce_th,
+                                           uint32_t& ce_d)
+{
     const long s0 = k * kCand, s1 = min(n, s0 + kCand);
     const float alpha = st->alpha, beta = st->beta;
     const uint32_t g_th = from_true ? st->theta : st->gth[gcur];
@@ -493,15 +637,16 @@ __device__ __forceinline__ void k_pll_cand_body(PllIn in, long n, AmpState* st, 
     } else {
         theta = g_th + (uint32_t)((uint64_t)w0 * d);   // constant-frequency extrapolation
     }
-    uint32_t nent = 0;
     if (approx) cand_warm_approx(in, w0, s0, alpha, beta, theta, d);
     else cand_run<false>(in, tab, w0, s0, alpha, beta, theta, d, cb, y, nent);
     cb.cs[2 * k] = theta;
     cb.cs[2 * k + 1] = d;
+    cs_th = theta, cs_d = d;
     cand_run<true>(in, tab, s0, s1, alpha, beta, theta, d, cb, y, nent);
     cb.ce[2 * k] = theta;
     cb.ce[2 * k + 1] = d;
     cb.cnt[k] = nent;
+    ce_th = theta, ce_d = d;
     if (k == cb.nchc - 1) {              // guess for the next call (other slot: every thread read [gcur])
         st->gth[1 - gcur] = theta;
         st->gd[1 - gcur] = d;
@@ -518,8 +663,9 @@ struct PllCandArgs {
     int warm;
     int from_true;
     int approx;
+    int fold;             // carrier: the chunk scan (k_pll_scan, flip 0) folded in
 };
-__device__ __forceinline__ void k_pll_cand_run(const PllCandArgs& a) { k_pll_cand_body(a.in, a.n, a.st, a.gcur, a.cb, a.y, a.warm, a.from_true, a.approx); }
+__device__ __forceinline__ void k_pll_cand_run(const PllCandArgs& a) { k_pll_cand_body(a.in, a.n, a.st, a.gcur, a.cb, a.y, a.warm, a.from_true, a.approx, a.fold); }
 LDSP_KERNEL_PAIR(k_pll_cand, PllCandArgs, k_pll_cand_run, 64)
 
 
@@ -1837,9 +1983,9 @@ LDSP_KERNEL_PAIR(k_delay_hist, DelayHistArgs, k_delay_hist_run, 64)
 } // namespace
 
 // Scratch layout (16-byte aligned pieces): phase words | cs | ce | cnt | eoff | pth | pd |
-// hk | ne | bbase | entries | entry outputs | stats (256 B).
+// hk | ne | bbase | entries | entry outputs | look-back granules | stats (256 B).
 struct PllLayout {
-    size_t rw, cs, ce, cnt, eoff, pth, pd, hk, ne, bbase, ent, eout, stats, total;
+    size_t rw, cs, ce, cnt, eoff, pth, pd, hk, ne, bbase, ent, eout, lb, stats, total;
     long nchc, nblkE;
 };
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -1862,6 +2008,7 @@ static PllLayout pll_layout(size_t n)
     L.bbase = o; o = al16(o + (size_t)L.nblkE * 4);
     L.ent = o;   o = al16(o + (size_t)L.nblkE * 2 * kBlkE * 16);
     L.eout = o;  o = al16(o + (size_t)L.nblkE * kBlkE * 4);
+    L.lb = o;    o = al16(o + (size_t)((nc + 63) / 64) * 6 * 8);
     L.stats = o; o += 256;
     L.total = o;
     return L;
@@ -1931,6 +2078,8 @@ static CandBuf cand_buf(const PllCall& c)
     cb.bbase = (uint32_t*)(p + L.bbase);
     cb.ent = (uint4*)(p + L.ent);
     cb.stats = (unsigned long long*)(p + L.stats);
+    cb.lb = (unsigned long long*)(p + L.lb);
+    cb.ep = 0u;
     cb.nchc = L.nchc;
     // risky margin B: with the carrier PLL |f| stays below 2^19 on ~99.6 % of the
     // samples of the AM chain (walker counters), and 2B / 2^22 = 1/4 of the samples
@@ -1958,7 +2107,19 @@ void pll_front(const PllCall& c, hipStream_t s)
     launch("k_delay_hist", k_delay_hist, k_delay_hist_many, dim3((unsigned)((c.m + 63) / 64)), dim3(64), 0, s,
            DelayHistArgs{(const float2*)c.x, (const float2*)c.hist, (float2*)c.hist_out, (long)c.n, c.m});
     if (!pll_parallel(c.n, c.costas)) return;
-    const CandBuf cb = cand_buf(c);
+    CandBuf cb = cand_buf(c);
+    // carrier: the chunk scan runs inside k_pll_cand (cand_scan_fold); Costas
+    // keeps the two scans around its re-flip
+    static const bool fold_knob = LDSP_KNOB("LDSP_PLL_FOLD", 1) != 0;
+    const bool fold = fold_knob && !c.costas;
+    if (fold) {
+        // a look-back epoch no granule in this process has carried (a random start:
+        // nor one left in reused device memory, but with 2^-32 odds)
+        static std::atomic<uint32_t> ep{(uint32_t)std::random_device{}() | 1u};
+        uint32_t e;
+        do e = ep.fetch_add(1u); while (e == 0u);
+        cb.ep = e;
+    }
     {
         static const int warm = LDSP_KNOB("LDSP_PLL_WARM", kWarm);
         // carrier loop: approximate warm-up (cand_warm_approx); Costas keeps the exact one
@@ -1966,14 +2127,14 @@ void pll_front(const PllCall& c, hipStream_t s)
         static const int approx = LDSP_KNOB("LDSP_PLL_WARM_APPROX", 1);
         launch("k_pll_cand", k_pll_cand, k_pll_cand_many, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s,
                PllCandArgs{pll_in(c), (long)c.n, c.st, c.gcur, cb, c.y, warm, c.costas,
-                           (approx && !c.costas) ? 1 : 0});
+                           (approx && !c.costas) ? 1 : 0, fold ? 1 : 0});
     }
     if (c.costas) {
         launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(kScanT), 0, s, PllScanArgs{cb, 1});
         launch("k_pll_reflip", k_pll_reflip, k_pll_reflip_many, dim3((unsigned)((cb.nchc + 63) / 64)), dim3(64), 0, s,
                PllReflipArgs{pll_in(c), (long)c.n, c.st, cb, c.y});
     }
-    launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(kScanT), 0, s, PllScanArgs{cb, 0});
+    if (!fold) launch("k_pll_scan", k_pll_scan, k_pll_scan_many, dim3(1), dim3(kScanT), 0, s, PllScanArgs{cb, 0});
     launch("k_pll_entries", k_pll_entries, k_pll_entries_many, dim3((unsigned)((cb.nchc + 3) / 4)), dim3(256), 0, s,
            PllEntriesArgs{pll_in(c), (const AmpState*)c.st, cb, (long)c.n});
 }
