@@ -548,13 +548,22 @@ __device__ __forceinline__ void cand_scan_fold(AmpState* st, const CandBuf& cb, 
             const long j = j0 - lane;
             uint32_t v0 = 0, v1 = 0, v2 = 0;
             int s = j >= 0 ? 0 : 3;                      // before chunk 0: an inclusive zero
+            bool first = true;
             for (;;) {
                 if (s == 0) {
+                    // the first read takes both records; a re-poll only the aggregate
+                    // (a predecessor publishes it first), with a pause long enough
+                    // that waiting lanes do not load the memory system the
+                    // concurrent kernels stream through
                     const unsigned long long* r = cb.lb + (size_t)j * 6;
                     unsigned long long q[6];
 #pragma unroll
-                    for (int e = 0; e < 6; e++) q[e] = __hip_atomic_load(r + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((q[3] >> 32) == cb.ep && (q[4] >> 32) == cb.ep && (q[5] >> 32) == cb.ep) {
+                    for (int e = 0; e < 3; e++) q[e] = __hip_atomic_load(r + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (first) {
+#pragma unroll
+                        for (int e = 3; e < 6; e++) q[e] = __hip_atomic_load(r + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (first && (q[3] >> 32) == cb.ep && (q[4] >> 32) == cb.ep && (q[5] >> 32) == cb.ep) {
                         s = 2;
                         v0 = (uint32_t)q[3], v1 = (uint32_t)q[4], v2 = (uint32_t)q[5];
                     } else if ((q[0] >> 32) == cb.ep && (q[1] >> 32) == cb.ep && (q[2] >> 32) == cb.ep) {
@@ -562,12 +571,13 @@ __device__ __forceinline__ void cand_scan_fold(AmpState* st, const CandBuf& cb, 
                         v0 = (uint32_t)q[0], v1 = (uint32_t)q[1], v2 = (uint32_t)q[2];
                     }
                 }
+                first = false;
                 const unsigned long long inc = __builtin_amdgcn_ballot_w64(s >= 2);
                 const int f = inc ? __builtin_ctzll(inc) : 64;
                 const unsigned long long need = f == 64 ? ~0ull : ((1ull << f) - 1ull);
                 if (!(__builtin_amdgcn_ballot_w64(s == 0) & need)) break;
                 if (wall_clock64() - tw > wmax) break;
-                __builtin_amdgcn_s_sleep(8);
+                __builtin_amdgcn_s_sleep(32);
             }
             const unsigned long long inc = __builtin_amdgcn_ballot_w64(s >= 2);
             const int f = inc ? __builtin_ctzll(inc) : 64;
@@ -2111,7 +2121,11 @@ void pll_front(const PllCall& c, hipStream_t s)
     // carrier: the chunk scan runs inside k_pll_cand (cand_scan_fold); Costas
     // keeps the two scans around its re-flip
     static const bool fold_knob = LDSP_KNOB("LDSP_PLL_FOLD", 1) != 0;
-    const bool fold = fold_knob && !c.costas;
+    // (not inside a many-call: there the scan is one merged launch for every
+    // object, and candidate workgroups that share CUs with the concurrent filter
+    // launches finish unevenly, so the look-back waits: 8 batched channels 2-5 %
+    // slower, scripts/fold_batched_ab.sh)
+    const bool fold = fold_knob && !c.costas && !batch_active();
     if (fold) {
         // a look-back epoch no granule in this process has carried (a random start:
         // nor one left in reused device memory, but with 2^-32 odds)
