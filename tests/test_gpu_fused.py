@@ -212,6 +212,36 @@ def test_filter_resample_64Mi_and_host(ld, rng):
     assert np.array_equal(bits(yh), bits(rb(fb(xh))))
 
 
+def test_filter_resample_rotating_streams(ld, rng):
+    """Consecutive fused calls on four rotating streams with no host sync: a
+    call's units start when the previous call's units end (the filter state),
+    under the previous call's edges, with the units' heads / tails in two
+    alternating side slots.  Seven calls (each slot reused three times, unit and
+    call boundaries of every kind), bit for bit against the two calls on one
+    stream, and the objects continue alike afterwards."""
+    import torch
+    n = 6 * 262_144 + 777
+    x = cgauss(rng, n)
+    xd = torch.from_numpy(x).cuda()
+    cuts = [0, 262_144, 300_000, 2 * 262_144 + 5, 3 * 262_144, 1_000_001, 5 * 262_144 + 64, n]
+    fa, ra = _iir_rs(ld, True)
+    fb, rb = _iir_rs(ld, True)
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    torch.cuda.synchronize()
+    ys = []
+    for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        with torch.cuda.stream(streams[i % 4]):        # ordered by the objects alone
+            ys.append(ld.filter_resample(fa, ra, xd[a:b]))
+    torch.cuda.synchronize()
+    refs = [rb(fb(xd[a:b])) for a, b in zip(cuts[:-1], cuts[1:])]
+    y, ref = torch.cat(ys).cpu().numpy(), torch.cat(refs).cpu().numpy()
+    assert y.shape == ref.shape and y.size > 0.023 * n
+    eq = bits(y) == bits(ref)
+    assert eq.all(), f"{(~eq).sum()} of {eq.size} differ; first at {int(np.argmin(eq))}"
+    x2 = torch.from_numpy(cgauss(rng, 50_000)).cuda()
+    assert torch.equal(ra(fa(x2)).view(torch.int32), rb(fb(x2)).view(torch.int32))
+
+
 @pytest.mark.parametrize("rate,fc", [(0.5, 0.2), (1.7, 0.3)])
 def test_filter_resample_other_rates(ld, rng, rate, fc):
     """Rates where a unit boundary is straddled by many resampler windows (the
