@@ -484,6 +484,22 @@ def test_ampmodem_walk_stats(ld, ora, rng):
     assert g._walk_stats()[0] >= 0
 
 
+def test_ampmodem_folded_scan_windows(ld, ora, rng):
+    """The carrier chunk scan folded into k_pll_cand (cand_scan_fold): a call of
+    193 candidate workgroups (the look-back reads its predecessors 64 at a time:
+    four windows), one whose last workgroup is full (chunks a multiple of 64) and
+    one whose last workgroup holds a single chunk -- the same output and state as
+    the restatement, bit for bit."""
+    sizes = [3 * 64 * 64 * 256 + 777, 3 * 64 * 256, 64 * 256 + 1]
+    x = _am(rng, sum(sizes), 48000.0, 300.0, amp=1.0)
+    g = ld.AmpModem(modulation=0.5, type="dsb", carrier=True)
+    o = ora.AmpModem(0.5, "dsb", carrier=True)
+    cuts = np.cumsum([0] + sizes)
+    y = np.concatenate([g(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert_bitwise(y, o(x))
+    assert g.pll_state() == o.pll_state
+
+
 @pytest.mark.parametrize("log2_b", [18, 17])
 def test_ampmodem_walk_fallbacks(ld, ora, rng, log2_b):
     # A narrower walker margin (2^19 by default) leaves gaps whose proofs fail:
