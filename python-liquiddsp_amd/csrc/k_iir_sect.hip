@@ -179,16 +179,37 @@ __device__ __forceinline__ void sect_run(const SectArgs& A)
         for (int k = 0; k < ntiles; k++) {
             const int slot = k & (kSR - 1);
             const int cnt = (int)min((long)kST, n - (long)k * kST);
+            const float* src = s == 0 ? xring + slot * kST : uscr0 + ((s - 1) * 2 + (k & 1)) * kST;
+            float* vo = ring + slot * kST;
+            const int c32 = cnt & ~31;
+            // The tile's first 32 inputs are read right behind the poll, under its
+            // round trip: one wave's LDS operations execute in order, so when the
+            // poll finds the tile published its data were written before these
+            // reads ran; if the poll fails they are read again after the wait.
+            float4 a0, a1v, a2v, a3, b0, b1, b2, b3;
             {
                 // both conditions polled with one ds_read_b64 (an LDS round trip is
                 // ~100 clocks, at every tile start); a wait only when either fails
                 const unsigned long long v = __hip_atomic_load(reinterpret_cast<unsigned long long*>(&sh.io[s]),
                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                asm volatile("" ::: "memory");
+                auto first = [&] {
+                    a0 = ld4(src), a1v = ld4(src + 4), a2v = ld4(src + 8), a3 = ld4(src + 12);
+                    b0 = ld4(src + 16), b1 = ld4(src + 20), b2 = ld4(src + 24), b3 = ld4(src + 28);
+                };
+                first();
+                // (kept here: not sunk below the poll's test by the compiler)
+#define SECT_PIN4(q) asm volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w))
+                SECT_PIN4(a0); SECT_PIN4(a1v); SECT_PIN4(a2v); SECT_PIN4(a3);
+                SECT_PIN4(b0); SECT_PIN4(b1); SECT_PIN4(b2); SECT_PIN4(b3);
+#undef SECT_PIN4
                 const int vin = __builtin_amdgcn_readfirstlane((int)(unsigned)v);
                 const int vout = __builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
                 if (vin < k + 1 || vout < k + 2 - kSR) {
                     ctr_wait<false>(&sh.io[s].x, k + 1, &sh.abort);
                     ctr_wait<false>(&sh.io[s].y, k + 2 - kSR, &sh.abort);
+                    asm volatile("" ::: "memory");
+                    first();
                 }
                 asm volatile("" ::: "memory");
             }
@@ -197,9 +218,6 @@ __device__ __forceinline__ void sect_run(const SectArgs& A)
                 c_wait += t - ca;
                 ca = t;
             }
-            const float* src = s == 0 ? xring + slot * kST : uscr0 + ((s - 1) * 2 + (k & 1)) * kST;
-            float* vo = ring + slot * kST;
-            const int c32 = cnt & ~31;
             // 32 samples per step in two register sets (a, b): the reads of one
             // set are issued before the other set's recursion, so they have landed
             // when it is needed.  The first step is peeled so that the loop is
@@ -210,35 +228,39 @@ __device__ __forceinline__ void sect_run(const SectArgs& A)
             // sample above the 26-clock chain (26.6-26.8 -> 25.8-26.1 measured).
             int i = 0;
             if (c32) {
-                float4 a0 = ld4(src), a1v = ld4(src + 4), a2v = ld4(src + 8), a3 = ld4(src + 12);
-                float4 b0 = ld4(src + 16), b1 = ld4(src + 20), b2 = ld4(src + 24), b3 = ld4(src + 28);
                 __builtin_amdgcn_sched_barrier(0);
-                auto step32 = [&](int i) {
+                auto step32 = [&](int i, bool pre) {      // pre: read the next step's inputs
                     group(a0, a1v, a2v, a3, vo + i);
-                    const int na = (i + 32) & (kST - 1);    // (the tile's start after the last)
-                    a0 = ld4(src + na);
-                    a1v = ld4(src + na + 4);
-                    a2v = ld4(src + na + 8);
-                    a3 = ld4(src + na + 12);
+                    if (pre) {
+                        a0 = ld4(src + i + 32);
+                        a1v = ld4(src + i + 36);
+                        a2v = ld4(src + i + 40);
+                        a3 = ld4(src + i + 44);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                     group(b0, b1, b2, b3, vo + i + 16);
-                    const int nb = (i + 48) & (kST - 1);
-                    b0 = ld4(src + nb);
-                    b1 = ld4(src + nb + 4);
-                    b2 = ld4(src + nb + 8);
-                    b3 = ld4(src + nb + 12);
+                    if (pre) {
+                        b0 = ld4(src + i + 48);
+                        b1 = ld4(src + i + 52);
+                        b2 = ld4(src + i + 56);
+                        b3 = ld4(src + i + 60);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                 };
-                step32(0);                                      // the peeled first iteration
+                // the peeled first step, then 128 samples per loop iteration (one back
+                // edge per 128), the tile's last step without reads past it
+                const int last = c32 - 32;
+                if (last > 0) step32(0, true);
                 i = 32;
-                // then 128 samples per loop iteration (one back edge per 128)
-                for (; i + 96 < c32; i += 128) {
-                    step32(i);
-                    step32(i + 32);
-                    step32(i + 64);
-                    step32(i + 96);
+                for (; i + 96 < last; i += 128) {
+                    step32(i, true);
+                    step32(i + 32, true);
+                    step32(i + 64, true);
+                    step32(i + 96, true);
                 }
-                for (; i < c32; i += 32) step32(i);
+                for (; i < last; i += 32) step32(i, true);
+                step32(last, false);
+                i = c32;
             }
             for (; i < cnt; i++) {
                 float v;
