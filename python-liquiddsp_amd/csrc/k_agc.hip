@@ -96,9 +96,10 @@ __device__ __forceinline__ float2 agc_step(AgcReg& r, const AgcState& p, float2 
 
 // Approximate step (hardware v_log_f32 / v_exp_f32, float32 smoothing): used
 // only to bring a chunk's guessed state within a few ulps of the true
-// trajectory before the exact warm-up (never for outputs).
+// trajectory before the exact warm-up (never for outputs).  kt = -alpha ln(2) / 2
+// (the caller's, loop-invariant).
 template <bool SQ>
-__device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, float2 x)
+__device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, float2 x, float kt)
 {
     const float a = x.x * r.g, b = x.y * r.g;
     const float y2 = a * a - b * (-b);
@@ -107,11 +108,13 @@ __device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, fl
     if (!p.locked) {
         // g *= expf(-0.5 alpha ln y2p) with the exact loop's rounding structure (factor
         // rounded to float, then one float multiply): ln from v_log_f32 (its error is
-        // scaled by alpha/2, far below an ulp of the factor), exp by a short series.  The
-        // factor then rounds like lm_expf's almost always, so this trajectory tracks the
-        // exact one within a few ulps instead of drifting by its own rounding noise.
-        const float t = -0.5f * p.alpha * (__builtin_amdgcn_logf(r.y2p) * 0.69314718056f);
-        const float u = t * (1.0f + t * (0.5f + t * (0.16666667f + t * 0.041666668f)));
+        // scaled by alpha/2, far below an ulp of the factor), exp by a short series
+        // in fused multiply-adds (its error ~1e-11, also far below that ulp).  The
+        // factor then rounds like lm_expf's almost always, so this trajectory tracks
+        // the exact one within a few ulps instead of drifting by its own rounding
+        // noise.
+        const float t = kt * __builtin_amdgcn_logf(r.y2p);
+        const float u = t * __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, 0.041666668f, 0.16666667f), 0.5f), 1.0f);
         r.g *= (r.y2p > 1e-6f) ? 1.0f + u : 1.0f;
         r.g = (r.g > 1e6f) ? 1e6f : r.g;
         if (SQ) agc_squelch(r, p);
@@ -122,8 +125,8 @@ __device__ __forceinline__ void agc_step_approx(AgcReg& r, const AgcState& p, fl
 // check (the lanes of a chunk kernel all run the same length, but the compiler
 // cannot know that: a per-sample check became an exec-mask branch around every
 // step), loads software-pipelined one batch ahead (addresses clamped, so the
-// prefetch needs no check either), then the tail sample by sample.  In a
-// one-wave dependent chain every instruction costs ~4 cycles of issue.
+// prefetch needs no check either), then the tail.  In a one-wave dependent
+// chain every instruction costs ~4 cycles of issue.
 template <bool SQ, class X>
 __device__ __forceinline__ void agc_run_approx_t(AgcReg& r, const AgcState& p, const X& x, long a, long b)
 {
@@ -132,6 +135,7 @@ __device__ __forceinline__ void agc_run_approx_t(AgcReg& r, const AgcState& p, c
 #endif
     constexpr int kA = LDSP_AGC_KA;
     if (a >= b) return;
+    const float kt = -0.5f * p.alpha * 0.69314718056f;
     const long full = a + (b - a) / kA * kA;
     float2 nx[kA];
 #pragma unroll
@@ -144,9 +148,9 @@ __device__ __forceinline__ void agc_run_approx_t(AgcReg& r, const AgcState& p, c
 #pragma unroll
         for (int j = 0; j < kA; j++) nx[j] = x[min(i + kA + j, b - 1)];
 #pragma unroll
-        for (int j = 0; j < kA; j++) agc_step_approx<SQ>(r, p, cx[j]);
+        for (int j = 0; j < kA; j++) agc_step_approx<SQ>(r, p, cx[j], kt);
     }
-    for (; i < b; i++) agc_step_approx<SQ>(r, p, x[i]);
+    for (; i < b; i++) agc_step_approx<SQ>(r, p, x[i], kt);
 }
 template <class X>
 __device__ __forceinline__ void agc_run_approx(AgcReg& r, const AgcState& p, const X& x, long a, long b)
